@@ -1,0 +1,439 @@
+/*
+ * pbn_oracle.c -- CPU restatement of the gym-PBN async update hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load this library, and only as the checker / the timed CPU
+ * baseline. The product (gym-pbn-stac_amd/) never links or calls it.
+ *
+ * Parity pinned: yes -- against golden vectors captured from the reference
+ * itself (tests/golden/make_golden.py), and the MT19937 stream against CPython's
+ * own `random` / numpy's legacy `RandomState` (tests/test_oracle.py).
+ *
+ * What it restates (reference file:line):
+ *   R1  Graph.step                      gym_PBN/envs/bittner/base.py:306-312
+ *   R2  Node.Predstep                   base.py:89-119 (selection by fp64
+ *       `random()*CODsum` vs cumulative COD, exactly as the reference; the
+ *       predictor output comes from the exported 16-entry table that was
+ *       evaluated with the reference's own np.matmul)
+ *   R3  flipNode / setState / genRandState  base.py:280-284,364-370
+ *   R4  PBN.step + Node.compute_next_value  common/pbn.py:129-133, common/node.py:31-38
+ *       (`u < p` in fp64 with u = k53 * 2^-53)
+ *   R6  PBNTargetMultiEnv.step          gym_PBN/envs/pbn_target_multi.py:119-154,
+ *       in_target :190-199, _get_reward :201-225, is_attracting_state :489-492
+ *   CPython random (MT19937, init_by_array seeding, getrandbits/_randbelow,
+ *   random()) -- the RNG the reference draws from (base.py:7,94,308); numpy
+ *   legacy RandomState (init_genrand seeding, random_sample) -- common/node.py:2,37.
+ *   Philox4x32-10 (Random123) -- the build-defined production stream, mapped to
+ *   (node, k53) identically to the HIP kernels (DESIGN.md "Philox mode").
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define EXPORT __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------ MT19937 */
+typedef struct {
+    uint32_t mt[624];
+    int idx;
+} orc_mt;
+
+EXPORT void orc_mt_init_genrand(orc_mt *s, uint32_t seed) {
+    s->mt[0] = seed;
+    for (int i = 1; i < 624; i++)
+        s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+    s->idx = 624;
+}
+
+EXPORT void orc_mt_init_by_array(orc_mt *s, const uint32_t *key, int klen) {
+    orc_mt_init_genrand(s, 19650218u);
+    int i = 1, j = 0;
+    int k = 624 > klen ? 624 : klen;
+    for (; k; k--) {
+        s->mt[i] = (s->mt[i] ^ ((s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        i++;
+        j++;
+        if (i >= 624) {
+            s->mt[0] = s->mt[623];
+            i = 1;
+        }
+        if (j >= klen) j = 0;
+    }
+    for (k = 623; k; k--) {
+        s->mt[i] = (s->mt[i] ^ ((s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= 624) {
+            s->mt[0] = s->mt[623];
+            i = 1;
+        }
+    }
+    s->mt[0] = 0x80000000u;
+    s->idx = 624;
+}
+
+/* random.seed(n) for a non-negative int n < 2^64 (CPython random_seed():
+ * key = 32-bit little-endian chunks of n, key = [0] for n == 0). */
+EXPORT void orc_mt_seed_python(orc_mt *s, uint64_t n) {
+    uint32_t key[2];
+    int klen;
+    key[0] = (uint32_t)n;
+    key[1] = (uint32_t)(n >> 32);
+    klen = key[1] ? 2 : 1;
+    orc_mt_init_by_array(s, key, klen);
+}
+
+/* np.random.seed(n) for 0 <= n < 2^32 (legacy mt19937_seed == init_genrand). */
+EXPORT void orc_mt_seed_numpy(orc_mt *s, uint32_t n) { orc_mt_init_genrand(s, n); }
+
+EXPORT uint32_t orc_mt_next(orc_mt *s) {
+    if (s->idx >= 624) {
+        int kk;
+        uint32_t y;
+        for (kk = 0; kk < 624 - 397; kk++) {
+            y = (s->mt[kk] & 0x80000000u) | (s->mt[kk + 1] & 0x7fffffffu);
+            s->mt[kk] = s->mt[kk + 397] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        for (; kk < 623; kk++) {
+            y = (s->mt[kk] & 0x80000000u) | (s->mt[kk + 1] & 0x7fffffffu);
+            s->mt[kk] = s->mt[kk + (397 - 624)] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        y = (s->mt[623] & 0x80000000u) | (s->mt[0] & 0x7fffffffu);
+        s->mt[623] = s->mt[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        s->idx = 0;
+    }
+    uint32_t y = s->mt[s->idx++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+/* random.random() == k53 * 2^-53; returns k53 */
+EXPORT uint64_t orc_mt_k53(orc_mt *s) {
+    uint32_t a = orc_mt_next(s) >> 5, b = orc_mt_next(s) >> 6;
+    return ((uint64_t)a << 26) | b;
+}
+
+static int bit_length(uint32_t n) { return n ? 32 - __builtin_clz(n) : 0; }
+
+/* Random._randbelow_with_getrandbits(n), 1 <= n < 2^32 (CPython 3.10 random.py) */
+EXPORT uint32_t orc_mt_randbelow(orc_mt *s, uint32_t n) {
+    int k = bit_length(n);
+    uint32_t r = orc_mt_next(s) >> (32 - k);
+    while (r >= n) r = orc_mt_next(s) >> (32 - k);
+    return r;
+}
+
+/* ------------------------------------------------------------ Philox4x32-10 */
+static inline void philox_round(uint32_t c[4], const uint32_t k[2]) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k[0], n2 = hi0 ^ c[3] ^ k[1];
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+}
+
+EXPORT void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr_in[0], ctr_in[1], ctr_in[2], ctr_in[3]};
+    uint32_t k[2] = {key_in[0], key_in[1]};
+    for (int r = 0; r < 10; r++) {
+        if (r) {
+            k[0] += 0x9E3779B9u;
+            k[1] += 0xBB67AE85u;
+        }
+        philox_round(c, k);
+    }
+    memcpy(out, c, sizeof c);
+}
+
+enum { STREAM_STEP = 1, STREAM_INIT = 2, STREAM_ENV = 3, STREAM_RESET = 4 };
+
+static inline void philox_draw(uint64_t seed, uint32_t c0, uint32_t c1, uint64_t gid, uint32_t stream,
+                               uint32_t out[4]) {
+    uint32_t ctr[4] = {c0, c1, (uint32_t)gid, (uint32_t)((gid >> 32) & 0xFFFFFFu) | (stream << 24)};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    orc_philox4x32_10(ctr, key, out);
+}
+
+/* ------------------------------------------------------------------ network */
+typedef struct {
+    int kind; /* 1 = predictor mix (Bittner), 2 = probability table (PBN) */
+    int n_nodes, n_words;
+    /* predictor mix */
+    const int32_t *pred_off;   /* [N+1] */
+    const int32_t *pred_in;    /* [P][3] */
+    const uint16_t *pred_tt;   /* [P] */
+    const double *pred_cum;    /* [P] cumulative COD */
+    const double *node_codsum; /* [N] */
+    /* prob table */
+    const int32_t *node_k;    /* [N] */
+    const int32_t *in_off;    /* [N+1] */
+    const int32_t *inputs;    /* [sum k] */
+    const int64_t *thr_off;   /* [N+1] */
+    const double *probs;      /* [sum 2^k] */
+} orc_net;
+
+static inline int getbit(const uint64_t *s, int i) { return (int)((s[i >> 6] >> (i & 63)) & 1u); }
+static inline void setbit(uint64_t *s, int i, int v) {
+    uint64_t m = (uint64_t)1 << (i & 63);
+    s[i >> 6] = v ? (s[i >> 6] | m) : (s[i >> 6] & ~m);
+}
+
+/* Node.Predstep (base.py:89-119) for node i with random() == k53*2^-53 */
+static inline int predstep(const orc_net *n, const uint64_t *s, int i, uint64_t k53) {
+    double r = ((double)k53 * 0x1p-53) * n->node_codsum[i]; /* base.py:94 */
+    int o0 = n->pred_off[i], o1 = n->pred_off[i + 1];
+    int j = o0;
+    for (; j < o1; j++) /* base.py:95-97: first predictor with COD > r */
+        if (n->pred_cum[j] > r) break;
+    if (j == o1) j = o1 - 1; /* loop fell through: Python keeps the last */
+    const int32_t *in = n->pred_in + 3 * j;
+    int p = (getbit(s, in[0]) << 3) | (getbit(s, in[1]) << 2) | (getbit(s, in[2]) << 1) | getbit(s, i);
+    return (n->pred_tt[j] >> p) & 1; /* base.py:110-118 via the exported table */
+}
+
+/* Node.compute_next_value (common/node.py:31-38): u < function.item(C-order index) */
+static inline int ttstep(const orc_net *n, const uint64_t *s, int i, uint64_t k53) {
+    int k = n->node_k[i];
+    const int32_t *in = n->inputs + n->in_off[i];
+    int64_t idx = 0;
+    for (int j = 0; j < k; j++) idx = (idx << 1) | getbit(s, in[j]);
+    double u = (double)k53 * 0x1p-53;
+    return u < n->probs[n->thr_off[i] + idx];
+}
+
+static inline int node_update(const orc_net *n, uint64_t *s, int i, uint64_t k53) {
+    int y = n->kind == 1 ? predstep(n, s, i, k53) : ttstep(n, s, i, k53);
+    setbit(s, i, y);
+    return y;
+}
+
+static inline int philox_node(const orc_net *n, uint32_t w0) {
+    if (n->kind == 1) return (int)(((uint64_t)w0 * (uint32_t)n->n_nodes) >> 32);
+    return 1 + (int)(((uint64_t)w0 * (uint32_t)(n->n_nodes - 1)) >> 32);
+}
+
+static inline uint64_t philox_k53(const uint32_t w[4]) { return ((uint64_t)(w[1] >> 5) << 26) | (w[2] >> 6); }
+
+/* --------------------------------------------------------------- step modes */
+/* Replay: node_idx/k53 are [T][B] (the draws the reference made). */
+EXPORT int orc_step_replay(const orc_net *n, uint64_t *state, int64_t B, const uint32_t *node_idx,
+                           const uint64_t *k53, int T) {
+    const int W = n->n_words;
+    for (int t = 0; t < T; t++)
+        for (int64_t e = 0; e < B; e++) {
+            uint32_t i = node_idx[(int64_t)t * B + e];
+            if ((int)i >= n->n_nodes) return -2;
+            node_update(n, state + e * W, (int)i, k53[(int64_t)t * B + e]);
+        }
+    return 0;
+}
+
+/* Philox: update u (global batch counter) of env with global id g draws
+ * philox(key=seed, ctr={u_lo, u_hi, g_lo, g_hi|STEP<<24}). */
+EXPORT int orc_step_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_t seed, uint64_t env_base,
+                           uint64_t update_base, int T, int n_threads) {
+    const int W = n->n_words;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t e = 0; e < B; e++) {
+        uint64_t s[64];
+        memcpy(s, state + e * W, 8 * (size_t)W);
+        uint64_t g = env_base + (uint64_t)e;
+        for (int t = 0; t < T; t++) {
+            uint64_t u = update_base + (uint64_t)t;
+            uint32_t w[4];
+            philox_draw(seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
+            node_update(n, s, philox_node(n, w[0]), philox_k53(w));
+        }
+        memcpy(state + e * W, s, 8 * (size_t)W);
+    }
+    return 0;
+}
+
+/* genRandState analogue for the Philox mode: fair bits, bits >= N cleared;
+ * probability-table networks also clear node 0 (pbn.py:118). */
+EXPORT void orc_init_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_t seed, uint64_t env_base,
+                            uint32_t reset_count) {
+    const int W = n->n_words;
+    for (int64_t e = 0; e < B; e++) {
+        uint64_t g = env_base + (uint64_t)e;
+        uint64_t *s = state + e * W;
+        for (int m = 0; 2 * m < W; m++) {
+            uint32_t w[4];
+            philox_draw(seed, (uint32_t)m, reset_count, g, STREAM_INIT, w);
+            s[2 * m] = ((uint64_t)w[1] << 32) | w[0];
+            if (2 * m + 1 < W) s[2 * m + 1] = ((uint64_t)w[3] << 32) | w[2];
+        }
+        int r = n->n_nodes & 63;
+        if (r) s[W - 1] &= (((uint64_t)1 << r) - 1);
+        if (n->kind == 2) s[0] &= ~(uint64_t)1;
+    }
+}
+
+/* MT mode, Bittner: per env e, random.seed(seeds[e]); genRandState(); T x Graph.step()
+ * (base.py:368-370, 306-312) -- exactly the reference's stream. */
+EXPORT int orc_bittner_run_mt(const orc_net *n, uint64_t *state, int64_t B, const uint64_t *seeds, int T,
+                              int do_init, int n_threads) {
+    const int W = n->n_words, N = n->n_nodes;
+    if (n->kind != 1) return -1;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t e = 0; e < B; e++) {
+        orc_mt mt;
+        orc_mt_seed_python(&mt, seeds[e]);
+        uint64_t *s = state + e * W;
+        if (do_init) {
+            memset(s, 0, 8 * (size_t)W);
+            for (int i = 0; i < N; i++) setbit(s, i, (int)orc_mt_randbelow(&mt, 2));
+        }
+        for (int t = 0; t < T; t++) {
+            int i = (int)orc_mt_randbelow(&mt, (uint32_t)N);
+            node_update(n, s, i, orc_mt_k53(&mt));
+        }
+    }
+    return 0;
+}
+
+/* MT mode, truth-table PBN: random.seed(s); np.random.seed(s); PBN.reset(); T x PBN.step()
+ * (pbn.py:96-133; reset draws np.random.rand(N) > 0.5, then state[0] = 0). */
+EXPORT int orc_tt_run_mt(const orc_net *n, uint64_t *state, int64_t B, const uint64_t *seeds, int T, int do_init,
+                         int n_threads) {
+    const int W = n->n_words, N = n->n_nodes;
+    if (n->kind != 2) return -1;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t e = 0; e < B; e++) {
+        orc_mt py, np_;
+        orc_mt_seed_python(&py, seeds[e]);
+        orc_mt_seed_numpy(&np_, (uint32_t)seeds[e]);
+        uint64_t *s = state + e * W;
+        if (do_init) {
+            memset(s, 0, 8 * (size_t)W);
+            for (int i = 0; i < N; i++) setbit(s, i, (double)orc_mt_k53(&np_) * 0x1p-53 > 0.5);
+            setbit(s, 0, 0);
+        }
+        for (int t = 0; t < T; t++) {
+            int i = 1 + (int)orc_mt_randbelow(&py, (uint32_t)(N - 1));
+            node_update(n, s, i, orc_mt_k53(&np_));
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------- R6 env step */
+typedef struct {
+    int n_cubes;
+    const uint64_t *care;  /* [H][W] */
+    const uint64_t *value; /* [H][W] */
+    const uint64_t *target_care, *target_value; /* [W]: all_attractors[-1][0] */
+    int horizon, reward_success, action_cost;
+} orc_envcfg;
+
+static inline int cube_match(const uint64_t *s, const uint64_t *care, const uint64_t *val, int W) {
+    for (int w = 0; w < W; w++)
+        if ((s[w] & care[w]) != val[w]) return 0;
+    return 1;
+}
+
+static inline int attracting(const orc_envcfg *c, const uint64_t *s, int W) {
+    for (int h = 0; h < c->n_cubes; h++)
+        if (cube_match(s, c->care + (int64_t)h * W, c->value + (int64_t)h * W, W)) return 1;
+    return 0;
+}
+
+/* Python list indexing of flipNode(a - offset): valid for -N <= idx < N. */
+static inline int action_node(int a, int offset, int N, int *node) {
+    int idx = a - offset;
+    if (idx >= N || idx < -N) return -1;
+    *node = idx < 0 ? idx + N : idx;
+    return 0;
+}
+
+/* rng_mode 0 = replay (draw_off [B+1], draws_i/draws_k), 1 = philox (seed, env_base, call_idx).
+ * flags bit0 terminated, bit1 truncated, bit2 capped. Returns -2 on an invalid action
+ * (checked for every env before any state changes). */
+EXPORT int orc_env_step_multi(const orc_net *n, const orc_envcfg *c, uint64_t *state, int64_t *n_steps, int64_t B,
+                              const int32_t *actions, int A, int dedup, int offset, int rng_mode,
+                              const int64_t *draw_off, const uint32_t *draws_i, const uint64_t *draws_k,
+                              uint64_t seed, uint64_t env_base, uint32_t call_idx, uint32_t update_cap,
+                              uint64_t *obs, int32_t *reward, uint8_t *flags, uint32_t *n_updates) {
+    const int W = n->n_words, N = n->n_nodes;
+    for (int64_t e = 0; e < B; e++)
+        for (int k = 0; k < A; k++) {
+            int a = actions[e * A + k], node;
+            if (a != 0 && action_node(a, offset, N, &node)) return -2;
+        }
+    for (int64_t e = 0; e < B; e++) {
+        uint64_t *s = state + e * W;
+        const int32_t *act = actions + e * A;
+        n_steps[e] += 1; /* :123 */
+        int n_act = 0;
+        for (int k = 0; k < A; k++) {
+            int a = act[k], dup = 0;
+            if (dedup)
+                for (int q = 0; q < k; q++) dup |= (act[q] == a);
+            if (dup) continue;
+            n_act++;
+            int node;
+            if (a != 0 && !action_node(a, offset, N, &node)) setbit(s, node, !getbit(s, node)); /* :125-127 */
+        }
+        uint64_t o[64];
+        memcpy(o, s, 8 * (size_t)W); /* :133 observation = getState() before the update */
+        uint32_t used = 0;
+        int capped = 0;
+        int64_t dpos = rng_mode == 0 ? draw_off[e] : 0;
+        for (;;) {
+            int i;
+            uint64_t k53;
+            if (used >= update_cap) {
+                capped = 1;
+                break;
+            }
+            if (rng_mode == 0) {
+                if (dpos >= draw_off[e + 1]) {
+                    capped = 1;
+                    break;
+                }
+                i = (int)draws_i[dpos];
+                k53 = draws_k[dpos];
+                dpos++;
+            } else {
+                uint32_t w[4];
+                philox_draw(seed, used, call_idx, env_base + (uint64_t)e, STREAM_ENV, w);
+                i = philox_node(n, w[0]);
+                k53 = philox_k53(w);
+            }
+            node_update(n, s, i, k53);
+            used++;
+            /* :134 the first update is never tested; :135-146 loop until obs is attracting */
+            if (used == 1) {
+                if (attracting(c, o, W)) break;
+            } else {
+                memcpy(o, s, 8 * (size_t)W);
+                if (attracting(c, o, W)) break;
+            }
+        }
+        memcpy(obs + e * W, o, 8 * (size_t)W);
+        int term = cube_match(o, c->target_care, c->target_value, W); /* :190-199 target[0] only */
+        reward[e] = (term ? c->reward_success : 0) - c->action_cost * (dedup ? n_act : A); /* :218-222 */
+        flags[e] = (uint8_t)(term | ((n_steps[e] == c->horizon) << 1) | (capped << 2));
+        n_updates[e] = used;
+    }
+    return 0;
+}
