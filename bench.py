@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the async PBN update on Bittner-200 at 1M envs per GPU.
+
+Workload (BASELINE.json configs[2], metric "env-steps/sec (whole node), Bittner-200,
+batch=1M; achieved HBM GB/s"): the exported ``predictor_sets_200_5_kmeans`` network
+(N=199 nodes, 994 predictors, W=4 state words), 1,048,576 independent envs per GPU
+resident in HBM as bit-packed uint64 words. One bench *step* = one R1 async
+transition (``Graph.step``, base.py:306-312) for every env = one ``pbn_step`` launch
+(state read from and written back to HBM). Philox4x32-10 RNG in-register.
+
+Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``):
+each rank owns 1,048,576 envs with global ids [rank*B, (rank+1)*B) -- weak scaling,
+no data-path collective (envs are independent); barrier + max-over-ranks timing.
+
+Prints ONE JSON line (rank 0) with ``roofline`` (algorithmic bytes / kernel time from
+HIP events on the batch stream) and ``cpu_baseline`` (the oracle's C restatement on
+host cores, rank 0 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--network", default="bittner199")
+    p.add_argument("--batch", type=int, default=1 << 20, help="envs per GPU")
+    p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-events", action="store_true", help="time without per-launch HIP events")
+    p.add_argument("--rollout", type=int, default=64, help="updates per launch for the supplementary rollout line")
+    p.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
+    return p.parse_args()
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return world, rank, local
+
+
+def cpu_baseline(net, seconds: float):
+    """Oracle (C restatement, same semantics and Philox stream) timed on host cores; bounded sample."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+
+    O.build()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    o = O.Oracle(net)
+    B = 65536
+    st = o.init_philox(B, seed=1)
+    T = 8
+    t0 = time.perf_counter()
+    o.step_philox(st, 1, 0, 0, T, n_threads=threads)
+    dt = time.perf_counter() - t0
+    T = max(8, int(T * seconds / max(dt, 1e-6)))
+    t0 = time.perf_counter()
+    o.step_philox(st, 1, 0, 0, T, n_threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": B * T / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/pbn_oracle.c orc_step_philox, {net.name}, {B} envs x {T} updates "
+                      f"({dt:.1f} s, OpenMP {threads} threads)",
+            "reference_python_1core_measured_in_build_container": "20-28k env-steps/s (BASELINE.md)"}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_env()
+    import numpy as np
+    import torch
+
+    from gym_pbn_amd import _lib
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.network import load_network
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = local if world > 1 else 0
+    if torch.cuda.is_available():
+        torch.cuda.set_device(device)
+
+    net = load_network(args.network)
+    B = args.batch
+    batch = PBNBatch(net, B, device=device, env_id_base=rank * B, seed=args.seed)
+    batch.randomize()
+    batch.sync()
+
+    if args.kernel_only:
+        batch.step(args.warmup + args.steps)
+        batch.sync()
+        return
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    batch.step(args.warmup)
+    batch.sync()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    if not args.no_events:
+        batch.timing(True)
+    t0 = time.perf_counter()
+    batch.step(args.steps)
+    batch.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    kernel_ms, launches = batch.timing_read() if not args.no_events else (float("nan"), 0)
+    batch.timing(False)
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=f"cuda:{device}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([kernel_ms], device=f"cuda:{device}", dtype=torch.float64)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kernel_ms = float(k.item())
+
+    # supplementary: rollout mode (several updates per launch, state in registers)
+    rollout = None
+    if args.rollout > 1:
+        batch.rollout(args.rollout)
+        batch.sync()
+        batch.timing(True)
+        reps = 5
+        for _ in range(reps):
+            batch.rollout(args.rollout)
+        rms, rl = batch.timing_read()
+        batch.timing(False)
+        rollout = {"updates_per_launch": args.rollout,
+                   "node_updates_per_s_per_gpu": B * args.rollout * reps / (rms / 1e3),
+                   "kernel_ms": rms / max(rl, 1)}
+
+    W = net.n_words
+    alg_bytes = 16 * W * B  # read + write the packed state of every env
+    avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
+    traffic = None
+    pmc_src = None
+    try:
+        pmc = json.loads(Path(args.pmc_file).read_text())
+        key = f"{args.network}:{B}"
+        if key in pmc.get("per_launch_bytes", {}):
+            traffic = pmc["per_launch_bytes"][key]
+            pmc_src = pmc.get("source")
+    except (OSError, ValueError):
+        pass
+
+    total_steps = world * B * args.steps
+    value = total_steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": "env-steps/sec (whole node), Bittner-200, batch=1M; achieved HBM GB/s",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (Philox fair-bit initial states; network exported from the reference's "
+                    "predictor_sets_200_5_kmeans.pkl)",
+            "config": {
+                "workload": "Bittner-200 async node update (R1 Graph.step), step mode: one update per env per "
+                            "launch, state resident in HBM",
+                "network": args.network, "n_nodes": net.n_nodes, "state_words": W,
+                "batch_per_gpu": B, "global_batch": world * B, "updates_per_step": 1,
+                "parallelism": f"dp{world} (env shards, no collective)", "rng": "philox4x32-10",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic,
+                "kernel": "pbn::k_step<4,1,STORE_DIRTY,0>",
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
+                "traffic_source": pmc_src,
+            },
+            "node_updates_per_s": value,
+            "rollout": rollout,
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(net, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    batch.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    del np, _lib
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,852 @@
+// pbn_abi.cpp -- host side of libpbnsim.so: the C ABI declared in include/pbn_abi.h.
+//
+// Owns device memory, validates descriptors, packs the network tables into the
+// LDS image the kernels stage, and drives the kernels on one HIP stream per batch.
+// There is no host compute path: every state transition runs on the GPU, and a
+// missing/unsupported device is reported as an error, never silently emulated.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pbn_abi.h"
+#include "pbn_params.hpp"
+
+using namespace pbn;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) return fail(PBN_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) return fail(PBN_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        cap = bytes;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct pbn_net {
+    int kind = 0, N = 0, W = 0;
+    std::vector<uint8_t> image;  // host copy of the LDS image
+    NetLayout L{};
+    std::mutex mu;
+    std::map<int, void*> dev_image;  // per device
+    const void* image_on(int device) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = dev_image.find(device);
+        if (it != dev_image.end()) return it->second;
+        void* p = nullptr;
+        if (hipMalloc(&p, image.size()) != hipSuccess) return nullptr;
+        if (hipMemcpy(p, image.data(), image.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        dev_image[device] = p;
+        return p;
+    }
+};
+
+struct pbn_envcfg {
+    const pbn_net* net = nullptr;
+    int W = 0, H = 0, H_reset = 0;
+    std::vector<uint8_t> image;  // net image + cubes [H][2][W] + target [2][W]
+    NetLayout L{};
+    uint32_t off_cubes = 0, off_target = 0;
+    std::vector<uint64_t> reset_care, reset_value;
+    int32_t horizon = 100, reward_success = 1000, action_cost = 1;
+    std::mutex mu;
+    struct Dev {
+        void* image = nullptr;
+        void* reset_care = nullptr;
+        void* reset_value = nullptr;
+    };
+    std::map<int, Dev> dev;
+    const Dev* on(int device) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = dev.find(device);
+        if (it != dev.end()) return &it->second;
+        Dev d;
+        size_t rb = reset_care.size() * 8;
+        if (hipMalloc(&d.image, image.size()) != hipSuccess) return nullptr;
+        if (hipMemcpy(d.image, image.data(), image.size(), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        if (rb) {
+            if (hipMalloc(&d.reset_care, rb) != hipSuccess || hipMalloc(&d.reset_value, rb) != hipSuccess)
+                return nullptr;
+            if (hipMemcpy(d.reset_care, reset_care.data(), rb, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(d.reset_value, reset_value.data(), rb, hipMemcpyHostToDevice) != hipSuccess)
+                return nullptr;
+        }
+        dev[device] = d;
+        return &dev[device];
+    }
+};
+
+struct pbn_batch {
+    pbn_net* net = nullptr;
+    int device = 0, W = 0, N = 0;
+    hipStream_t stream = nullptr;
+    uint64_t B = 0, env_base = 0, seed = 0, update_count = 0;
+    uint32_t env_calls = 0, reset_count = 0;
+    uint64_t* d_state = nullptr;
+    int64_t* d_nsteps = nullptr;
+    int32_t* d_error = nullptr;
+    const void* d_image = nullptr;
+    int n_cu = 0, bpc_step = 1, bpc_env = 1;
+    int store_mode = STORE_DIRTY;
+    DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
+    // timing
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    size_t ev_used = 0;
+    int mt_ready = 0;
+
+    int grid_for(uint64_t items, int bpc) const {
+        uint64_t need = (items + BLOCK - 1) / BLOCK;
+        uint64_t cap = (uint64_t)n_cu * (uint64_t)bpc;
+        uint64_t g = std::min<uint64_t>(need, cap);
+        return (int)std::max<uint64_t>(g, 1);
+    }
+    int grid_all(uint64_t items) const { return (int)std::max<uint64_t>((items + BLOCK - 1) / BLOCK, 1); }
+    int ev_begin(hipEvent_t* stop) {
+        *stop = nullptr;
+        if (!timing) return 0;
+        if (ev_used == ev_pool.size()) {
+            hipEvent_t a, b;
+            HIP_TRY(hipEventCreate(&a));
+            HIP_TRY(hipEventCreate(&b));
+            ev_pool.emplace_back(a, b);
+        }
+        auto& pr = ev_pool[ev_used++];
+        HIP_TRY(hipEventRecord(pr.first, stream));
+        *stop = pr.second;
+        return 0;
+    }
+    int ev_end(hipEvent_t stop) {
+        if (stop) HIP_TRY(hipEventRecord(stop, stream));
+        return 0;
+    }
+};
+
+#define CHECK_NN(p, name) \
+    if (!(p)) return fail(PBN_E_INVALID, "%s is NULL", name)
+#define SET_DEV(b) HIP_TRY(hipSetDevice((b)->device))
+
+static int build_predictor_image(const pbn_net_desc* d, pbn_net* n) {
+    const int N = d->n_nodes, P = d->n_preds;
+    CHECK_NN(d->pred_offsets, "pred_offsets");
+    CHECK_NN(d->pred_inputs, "pred_inputs");
+    CHECK_NN(d->pred_tt, "pred_tt");
+    CHECK_NN(d->pred_thr, "pred_thr");
+    if (P < 1 || P > 65535) return fail(PBN_E_UNSUPPORTED, "n_preds=%d outside [1, 65535]", P);
+    if (d->pred_offsets[0] != 0 || d->pred_offsets[N] != P) return fail(PBN_E_INVALID, "pred_offsets must span [0, P]");
+    for (int i = 0; i < N; i++) {
+        int c = d->pred_offsets[i + 1] - d->pred_offsets[i];
+        if (c < 1) return fail(PBN_E_INVALID, "node %d has no predictors (Predstep would fail, base.py:95-104)", i);
+        for (int j = d->pred_offsets[i] + 1; j < d->pred_offsets[i + 1]; j++)
+            if (d->pred_thr[j] < d->pred_thr[j - 1]) return fail(PBN_E_INVALID, "pred_thr not non-decreasing at node %d", i);
+    }
+    for (int j = 0; j < 3 * P; j++)
+        if (d->pred_inputs[j] < 0 || d->pred_inputs[j] >= N)
+            return fail(PBN_E_RANGE, "predictor input %d out of range [0, %d)", d->pred_inputs[j], N);
+    NetLayout L{};
+    L.off_node = 0;
+    L.off_thr = align16(4u * (uint32_t)N);
+    L.off_rec = align16(L.off_thr + 8u * (uint32_t)P);
+    L.bytes = align16(L.off_rec + 8u * (uint32_t)P);
+    L.kind = KIND_PREDICTOR_MIX;
+    L.n_nodes = N;
+    if (L.bytes > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "network tables (%u B) exceed the LDS budget", L.bytes);
+    n->image.assign(L.bytes, 0);
+    uint8_t* im = n->image.data();
+    for (int i = 0; i < N; i++) {
+        uint32_t o0 = (uint32_t)d->pred_offsets[i], c = (uint32_t)(d->pred_offsets[i + 1] - d->pred_offsets[i]);
+        uint32_t v = o0 | (c << 16);
+        memcpy(im + L.off_node + 4 * i, &v, 4);
+    }
+    for (int j = 0; j < P; j++) {
+        memcpy(im + L.off_thr + 8 * j, &d->pred_thr[j], 8);
+        uint64_t rec = (uint64_t)(uint32_t)d->pred_inputs[3 * j] | ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 1] << 16) |
+                       ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 2] << 32) | ((uint64_t)d->pred_tt[j] << 48);
+        memcpy(im + L.off_rec + 8 * j, &rec, 8);
+    }
+    n->L = L;
+    return 0;
+}
+
+static int build_table_image(const pbn_net_desc* d, pbn_net* n) {
+    const int N = d->n_nodes;
+    CHECK_NN(d->node_k, "node_k");
+    CHECK_NN(d->input_offsets, "input_offsets");
+    CHECK_NN(d->thr_offsets, "thr_offsets");
+    CHECK_NN(d->thr, "thr");
+    if (N < 2) return fail(PBN_E_INVALID, "a PBN needs N >= 2 (node 0 is never updated, pbn.py:131)");
+    int64_t sum_k = 0, sum_t = 0;
+    for (int i = 0; i < N; i++)
+        if (d->node_k[i] > 0 && !d->inputs) return fail(PBN_E_INVALID, "inputs is NULL");
+    for (int i = 0; i < N; i++) {
+        int k = d->node_k[i];
+        if (k < 0 || k > 16) return fail(PBN_E_UNSUPPORTED, "node %d has %d inputs (max 16)", i, k);
+        if (d->input_offsets[i] != sum_k) return fail(PBN_E_INVALID, "input_offsets inconsistent at node %d", i);
+        if (d->thr_offsets[i] != sum_t) return fail(PBN_E_INVALID, "thr_offsets inconsistent at node %d", i);
+        for (int q = 0; q < k; q++) {
+            int in = d->inputs[sum_k + q];
+            if (in < 0 || in >= N) return fail(PBN_E_RANGE, "input %d of node %d out of range", in, i);
+        }
+        sum_k += k;
+        sum_t += (int64_t)1 << k;
+    }
+    NetLayout L{};
+    L.off_node = 0;
+    L.off_rec = align16(8u * (uint32_t)N);
+    uint64_t after_in = L.off_rec + 2u * (uint64_t)sum_k;
+    if (after_in > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "input lists exceed the LDS budget");
+    L.off_thr = align16((uint32_t)after_in);
+    uint64_t total = (uint64_t)L.off_thr + 8u * (uint64_t)sum_t;
+    if (total > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "probability tables (%llu B) exceed the LDS budget",
+                                       (unsigned long long)total);
+    L.bytes = align16((uint32_t)total);
+    L.kind = KIND_PROB_TABLE;
+    L.n_nodes = N;
+    n->image.assign(L.bytes, 0);
+    uint8_t* im = n->image.data();
+    for (int i = 0; i < N; i++) {
+        uint64_t v = (uint64_t)(uint32_t)d->thr_offsets[i] | ((uint64_t)(uint32_t)d->input_offsets[i] << 32) |
+                     ((uint64_t)(uint32_t)d->node_k[i] << 48);
+        memcpy(im + L.off_node + 8 * i, &v, 8);
+    }
+    for (int64_t q = 0; q < sum_k; q++) {
+        uint16_t v = (uint16_t)d->inputs[q];
+        memcpy(im + L.off_rec + 2 * q, &v, 2);
+    }
+    memcpy(im + L.off_thr, d->thr, 8 * (size_t)sum_t);
+    n->L = L;
+    return 0;
+}
+
+extern "C" {
+
+int pbn_abi_version(void) { return PBN_ABI_VERSION; }
+
+const char* pbn_last_error(void) { return g_err.c_str(); }
+
+int pbn_device_count(int* count) {
+    CHECK_NN(count, "count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(PBN_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return 0;
+}
+
+int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
+    CHECK_NN(d, "desc");
+    CHECK_NN(out, "out");
+    *out = nullptr;
+    if (d->n_nodes < 1 || d->n_nodes > 64 * MAX_WORDS)
+        return fail(PBN_E_UNSUPPORTED, "n_nodes=%d outside [1, %d]", d->n_nodes, 64 * MAX_WORDS);
+    pbn_net* n = new pbn_net;
+    n->kind = d->kind;
+    n->N = d->n_nodes;
+    n->W = (d->n_nodes + 63) / 64;
+    int rc;
+    if (d->kind == PBN_KIND_PREDICTOR_MIX)
+        rc = build_predictor_image(d, n);
+    else if (d->kind == PBN_KIND_PROB_TABLE)
+        rc = build_table_image(d, n);
+    else
+        rc = fail(PBN_E_INVALID, "unknown network kind %d", d->kind);
+    if (rc) {
+        delete n;
+        return rc;
+    }
+    *out = n;
+    return 0;
+}
+
+void pbn_net_destroy(pbn_net* n) {
+    if (!n) return;
+    for (auto& kv : n->dev_image) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
+    }
+    delete n;
+}
+
+int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
+                     pbn_batch** out) {
+    CHECK_NN(net_c, "net");
+    CHECK_NN(out, "out");
+    *out = nullptr;
+    pbn_net* net = const_cast<pbn_net*>(net_c);
+    if (n_envs < 1) return fail(PBN_E_INVALID, "n_envs must be >= 1");
+    if (env_id_base + n_envs > ((uint64_t)1 << 56)) return fail(PBN_E_RANGE, "global env ids must stay below 2^56");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev < 1)
+        return fail(PBN_E_HIP, "no HIP device available (hipGetDeviceCount: %s); libpbnsim has no CPU path",
+                    hipGetErrorString(e));
+    if (device < 0 || device >= ndev) return fail(PBN_E_RANGE, "device %d outside [0, %d)", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    pbn_batch* b = new pbn_batch;
+    b->net = net;
+    b->device = device;
+    b->W = net->W;
+    b->N = net->N;
+    b->B = n_envs;
+    b->env_base = env_id_base;
+    b->seed = seed;
+    if (const char* sm = getenv("PBNSIM_STORE_MODE")) b->store_mode = atoi(sm) ? STORE_DIRTY : STORE_FULL;
+    hipDeviceProp_t prop;
+    int rc = 0;
+    auto bail = [&](int code) {
+        pbn_batch_destroy(b);
+        return code;
+    };
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PBN_E_HIP, "hipGetDeviceProperties"));
+    b->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(PBN_E_HIP, "hipStreamCreate"));
+    size_t sb = 8 * (size_t)b->W * n_envs;
+    if (hipMalloc(&b->d_state, sb) != hipSuccess) return bail(fail(PBN_E_NOMEM, "state alloc (%zu B)", sb));
+    if (hipMalloc(&b->d_nsteps, 8 * n_envs) != hipSuccess) return bail(fail(PBN_E_NOMEM, "n_steps alloc"));
+    if (hipMalloc(&b->d_error, 4) != hipSuccess) return bail(fail(PBN_E_NOMEM, "error flag alloc"));
+    if (hipMemsetAsync(b->d_state, 0, sb, b->stream) != hipSuccess ||
+        hipMemsetAsync(b->d_nsteps, 0, 8 * n_envs, b->stream) != hipSuccess)
+        return bail(fail(PBN_E_HIP, "hipMemset"));
+    b->d_image = net->image_on(device);
+    if (!b->d_image) return bail(fail(PBN_E_NOMEM, "network image upload failed"));
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, &b->bpc_step)))
+        return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
+    if (hipStreamSynchronize(b->stream) != hipSuccess) return bail(fail(PBN_E_HIP, "stream sync"));
+    *out = b;
+    return 0;
+}
+
+void pbn_batch_destroy(pbn_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (auto& pr : b->ev_pool) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    if (b->d_state) (void)hipFree(b->d_state);
+    if (b->d_nsteps) (void)hipFree(b->d_nsteps);
+    if (b->d_error) (void)hipFree(b->d_error);
+    for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
+                      &b->s_off, &b->s_mask})
+        d->release();
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(info, "info");
+    info->n_nodes = b->N;
+    info->n_words = b->W;
+    info->kind = b->net->kind;
+    info->device = b->device;
+    info->n_envs = b->B;
+    info->env_id_base = b->env_base;
+    info->seed = b->seed;
+    info->update_count = b->update_count;
+    info->env_call_count = b->env_calls;
+    info->reset_count = b->reset_count;
+    info->mt_ready = b->mt_ready;
+    return 0;
+}
+
+int pbn_sync(pbn_batch* b) {
+    CHECK_NN(b, "batch");
+    SET_DEV(b);
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+static int check_state_words(const pbn_batch* b, const uint64_t* w) {
+    const int r = b->N & 63;
+    if (!r) return 0;
+    const uint64_t bad = ~(((uint64_t)1 << r) - 1);
+    for (uint64_t e = 0; e < b->B; e++)
+        if (w[e * b->W + b->W - 1] & bad) return fail(PBN_E_RANGE, "env %llu has bits set beyond node %d",
+                                                       (unsigned long long)e, b->N - 1);
+    return 0;
+}
+
+int pbn_set_state(pbn_batch* b, const uint64_t* words) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(words, "words");
+    if (int rc = check_state_words(b, words)) return rc;
+    SET_DEV(b);
+    HIP_TRY(hipMemcpyAsync(b->d_state, words, 8 * (size_t)b->W * b->B, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_get_state(pbn_batch* b, uint64_t* words) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(words, "words");
+    SET_DEV(b);
+    HIP_TRY(hipMemcpyAsync(words, b->d_state, 8 * (size_t)b->W * b->B, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_set_state_device(pbn_batch* b, const void* dev_words) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(dev_words, "dev_words");
+    SET_DEV(b);
+    HIP_TRY(hipMemcpyAsync(b->d_state, dev_words, 8 * (size_t)b->W * b->B, hipMemcpyDeviceToDevice, b->stream));
+    return 0;
+}
+
+int pbn_get_state_device(pbn_batch* b, void* dev_words) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(dev_words, "dev_words");
+    SET_DEV(b);
+    HIP_TRY(hipMemcpyAsync(dev_words, b->d_state, 8 * (size_t)b->W * b->B, hipMemcpyDeviceToDevice, b->stream));
+    return 0;
+}
+
+static int run_init(pbn_batch* b, const pbn_envcfg* cfg, const void* d_mask, const void* care, const void* value) {
+    InitArgs a{};
+    a.state = b->d_state;
+    a.B = b->B;
+    a.env_base = b->env_base;
+    a.seed = b->seed;
+    a.reset_count = b->reset_count;
+    a.n_nodes = b->N;
+    a.kind = b->net->kind;
+    a.cube_care = (const uint64_t*)care;
+    a.cube_value = (const uint64_t*)value;
+    a.n_cubes = cfg ? cfg->H_reset : 0;
+    a.mask = (const uint8_t*)d_mask;
+    a.n_steps = cfg ? b->d_nsteps : nullptr;
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int e = launch_init(b->W, a, b->grid_all(b->B), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_init launch: %s", hipGetErrorString((hipError_t)e));
+    if (int rc = b->ev_end(stop)) return rc;
+    b->reset_count++;
+    return 0;
+}
+
+int pbn_randomize_state(pbn_batch* b) {
+    CHECK_NN(b, "batch");
+    SET_DEV(b);
+    return run_init(b, nullptr, nullptr, nullptr, nullptr);
+}
+
+static int validate_actions(const pbn_batch* b, const int32_t* actions, int A, int offset) {
+    if (A < 1 || A > 4096) return fail(PBN_E_INVALID, "A=%d outside [1, 4096]", A);
+    if (offset != 0 && offset != 1) return fail(PBN_E_INVALID, "offset must be 0 or 1");
+    const uint64_t n = b->B * (uint64_t)A;
+    for (uint64_t k = 0; k < n; k++) {
+        int32_t v = actions[k];
+        if (v == 0) continue;
+        int32_t idx = v - offset;
+        if (idx >= b->N || idx < -b->N)
+            return fail(PBN_E_RANGE, "Invalid action, no node at index %d (env %llu)", idx,
+                        (unsigned long long)(k / A));  // base.py:283-284
+    }
+    return 0;
+}
+
+int pbn_flip(pbn_batch* b, const int32_t* actions, int A, int offset, int dedup) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(actions, "actions");
+    if (int rc = validate_actions(b, actions, A, offset)) return rc;
+    SET_DEV(b);
+    size_t bytes = 4 * (size_t)A * b->B;
+    if (int rc = b->s_act.ensure(bytes)) return rc;
+    HIP_TRY(hipMemcpyAsync(b->s_act.p, actions, bytes, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemsetAsync(b->d_error, 0, 4, b->stream));
+    FlipArgs a{b->d_state, (const int32_t*)b->s_act.p, b->B, A, offset, dedup ? 1 : 0, b->N, b->d_error};
+    int e = launch_flip(b->W, a, b->grid_all(b->B), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_flip launch: %s", hipGetErrorString((hipError_t)e));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int replay, const void* d_i, const void* d_k) {
+    StepArgs a{};
+    a.state = b->d_state;
+    a.img = b->d_image;
+    a.L = b->net->L;
+    a.B = b->B;
+    a.env_base = b->env_base;
+    a.seed = b->seed;
+    a.update_base = update_base;
+    a.T = T;
+    a.replay_node = (const uint32_t*)d_i;
+    a.replay_k53 = (const uint64_t*)d_k;
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int store = (T == 1 && !replay) ? b->store_mode : STORE_FULL;
+    int e = launch_step(b->W, a, store, replay, b->grid_for(b->B, b->bpc_step), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_step launch: %s", hipGetErrorString((hipError_t)e));
+    return b->ev_end(stop);
+}
+
+int pbn_step(pbn_batch* b, uint32_t n_updates) {
+    CHECK_NN(b, "batch");
+    SET_DEV(b);
+    for (uint32_t t = 0; t < n_updates; t++) {
+        if (int rc = step_launch(b, 1, b->update_count, 0, nullptr, nullptr)) return rc;
+        b->update_count++;
+    }
+    return 0;
+}
+
+int pbn_rollout(pbn_batch* b, uint32_t n_updates) {
+    CHECK_NN(b, "batch");
+    if (!n_updates) return 0;
+    SET_DEV(b);
+    if (int rc = step_launch(b, n_updates, b->update_count, 0, nullptr, nullptr)) return rc;
+    b->update_count += n_updates;
+    return 0;
+}
+
+int pbn_step_replay(pbn_batch* b, const uint32_t* node_idx, const uint64_t* k53, uint32_t n_updates) {
+    CHECK_NN(b, "batch");
+    if (!n_updates) return 0;
+    CHECK_NN(node_idx, "node_idx");
+    CHECK_NN(k53, "k53");
+    const uint64_t n = (uint64_t)n_updates * b->B;
+    const uint32_t lo = (uint32_t)b->net->kind == PBN_KIND_PROB_TABLE ? 1u : 0u;
+    for (uint64_t q = 0; q < n; q++) {
+        if (node_idx[q] >= (uint32_t)b->N || node_idx[q] < lo)
+            return fail(PBN_E_RANGE, "replay node index %u outside [%u, %d)", node_idx[q], lo, b->N);
+        if (k53[q] >> 53) return fail(PBN_E_RANGE, "replay k53 must be < 2^53");
+    }
+    SET_DEV(b);
+    if (int rc = b->s_replay_i.ensure(4 * n)) return rc;
+    if (int rc = b->s_replay_k.ensure(8 * n)) return rc;
+    HIP_TRY(hipMemcpyAsync(b->s_replay_i.p, node_idx, 4 * n, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->s_replay_k.p, k53, 8 * n, hipMemcpyHostToDevice, b->stream));
+    if (int rc = step_launch(b, n_updates, 0, 1, b->s_replay_i.p, b->s_replay_k.p)) return rc;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_mt_seed(pbn_batch* b, const uint64_t* seeds, int init_state) {
+    (void)seeds;
+    (void)init_state;
+    CHECK_NN(b, "batch");
+    return fail(PBN_E_UNSUPPORTED, "MT mode is not built into this library version");
+}
+
+int pbn_mt_step(pbn_batch* b, uint32_t n_updates) {
+    (void)n_updates;
+    CHECK_NN(b, "batch");
+    if (!b->mt_ready) return fail(PBN_E_STATE, "pbn_mt_seed has not been called");
+    return fail(PBN_E_UNSUPPORTED, "MT mode is not built into this library version");
+}
+
+// ------------------------------------------------------------------ R6 env
+int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg** out) {
+    CHECK_NN(net, "net");
+    CHECK_NN(d, "desc");
+    CHECK_NN(out, "out");
+    *out = nullptr;
+    const int W = net->W;
+    if (d->n_cubes < 0 || d->n_cubes > 4096) return fail(PBN_E_INVALID, "n_cubes=%d outside [0, 4096]", d->n_cubes);
+    if (d->n_cubes && (!d->cube_care || !d->cube_value)) return fail(PBN_E_INVALID, "cube arrays are NULL");
+    if (d->n_reset_cubes < 0 || (d->n_reset_cubes && (!d->reset_care || !d->reset_value)))
+        return fail(PBN_E_INVALID, "bad reset cubes");
+    CHECK_NN(d->target_care, "target_care");
+    CHECK_NN(d->target_value, "target_value");
+    pbn_envcfg* c = new pbn_envcfg;
+    c->net = net;
+    c->W = W;
+    c->H = d->n_cubes;
+    c->H_reset = d->n_reset_cubes;
+    c->L = net->L;
+    c->off_cubes = net->L.bytes;
+    c->off_target = align16(c->off_cubes + 16u * (uint32_t)W * (uint32_t)c->H);
+    uint32_t bytes = align16(c->off_target + 16u * (uint32_t)W);
+    if (bytes > MAX_IMAGE) {
+        delete c;
+        return fail(PBN_E_UNSUPPORTED, "network + %d attractor cubes exceed the LDS budget", d->n_cubes);
+    }
+    c->image.assign(bytes, 0);
+    memcpy(c->image.data(), net->image.data(), net->image.size());
+    uint64_t* cubes = reinterpret_cast<uint64_t*>(c->image.data() + c->off_cubes);
+    for (int h = 0; h < c->H; h++)
+        for (int k = 0; k < W; k++) {
+            uint64_t care = d->cube_care[(size_t)h * W + k];
+            cubes[(size_t)h * 2 * W + k] = care;
+            cubes[(size_t)h * 2 * W + W + k] = d->cube_value[(size_t)h * W + k] & care;
+        }
+    uint64_t* tgt = reinterpret_cast<uint64_t*>(c->image.data() + c->off_target);
+    for (int k = 0; k < W; k++) {
+        tgt[k] = d->target_care[k];
+        tgt[W + k] = d->target_value[k] & d->target_care[k];
+    }
+    c->L.bytes = bytes;
+    c->reset_care.assign(d->reset_care, d->reset_care + (size_t)c->H_reset * W);
+    c->reset_value.assign(d->reset_value, d->reset_value + (size_t)c->H_reset * W);
+    c->horizon = d->horizon;
+    c->reward_success = d->reward_success;
+    c->action_cost = d->action_cost;
+    *out = c;
+    return 0;
+}
+
+void pbn_envcfg_destroy(pbn_envcfg* c) {
+    if (!c) return;
+    for (auto& kv : c->dev) {
+        (void)hipSetDevice(kv.first);
+        if (kv.second.image) (void)hipFree(kv.second.image);
+        if (kv.second.reset_care) (void)hipFree(kv.second.reset_care);
+        if (kv.second.reset_value) (void)hipFree(kv.second.reset_value);
+    }
+    delete c;
+}
+
+int pbn_env_reset(pbn_batch* b, const pbn_envcfg* cfg_c, const uint8_t* mask) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(cfg_c, "cfg");
+    pbn_envcfg* cfg = const_cast<pbn_envcfg*>(cfg_c);
+    if (cfg->net != b->net) return fail(PBN_E_INVALID, "envcfg belongs to another network");
+    if (cfg->H_reset < 1) return fail(PBN_E_STATE, "envcfg has no reset cubes (all_attractors[0])");
+    SET_DEV(b);
+    const pbn_envcfg::Dev* dv = cfg->on(b->device);
+    if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
+    const void* d_mask = nullptr;
+    if (mask) {
+        if (int rc = b->s_mask.ensure(b->B)) return rc;
+        HIP_TRY(hipMemcpyAsync(b->s_mask.p, mask, b->B, hipMemcpyHostToDevice, b->stream));
+        d_mask = b->s_mask.p;
+    }
+    if (int rc = run_init(b, cfg, d_mask, dv->reset_care, dv->reset_value)) return rc;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_set_n_steps(pbn_batch* b, const int64_t* n_steps) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(n_steps, "n_steps");
+    SET_DEV(b);
+    HIP_TRY(hipMemcpyAsync(b->d_nsteps, n_steps, 8 * b->B, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_get_n_steps(pbn_batch* b, int64_t* n_steps) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(n_steps, "n_steps");
+    SET_DEV(b);
+    HIP_TRY(hipMemcpyAsync(n_steps, b->d_nsteps, 8 * b->B, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A, int dedup, int offset,
+                      uint32_t cap, uint64_t* d_obs, int32_t* d_rew, uint8_t* d_flags, uint32_t* d_nup, int replay,
+                      const void* d_off, const void* d_di, const void* d_dk) {
+    const pbn_envcfg::Dev* dv = cfg->on(b->device);
+    if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
+    int bpc = 1;
+    if (int e = max_blocks_env(b->W, b->net->kind, cfg->L.bytes, &bpc))
+        return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
+    EnvArgs a{};
+    a.state = b->d_state;
+    a.n_steps = b->d_nsteps;
+    a.actions = d_act;
+    a.obs = d_obs;
+    a.reward = d_rew;
+    a.flags = d_flags;
+    a.n_updates = d_nup;
+    a.error = b->d_error;
+    a.img = dv->image;
+    a.L = cfg->L;
+    a.off_cubes = cfg->off_cubes;
+    a.off_target = cfg->off_target;
+    a.n_cubes = cfg->H;
+    a.B = b->B;
+    a.env_base = b->env_base;
+    a.seed = b->seed;
+    a.call_idx = b->env_calls;
+    a.update_cap = cap;
+    a.A = A;
+    a.offset = offset;
+    a.dedup = dedup ? 1 : 0;
+    a.horizon = cfg->horizon;
+    a.reward_success = cfg->reward_success;
+    a.action_cost = cfg->action_cost;
+    a.draw_off = (const int64_t*)d_off;
+    a.draws_i = (const uint32_t*)d_di;
+    a.draws_k = (const uint64_t*)d_dk;
+    HIP_TRY(hipMemsetAsync(b->d_error, 0, 4, b->stream));
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int e = launch_env_multi(b->W, a, replay, b->grid_for(b->B, bpc), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_env launch: %s", hipGetErrorString((hipError_t)e));
+    if (int rc = b->ev_end(stop)) return rc;
+    if (!replay) b->env_calls++;
+    return 0;
+}
+
+static int env_host_common(pbn_batch* b, pbn_envcfg* cfg, const int32_t* actions, int A, int offset) {
+    if (cfg->net != b->net) return fail(PBN_E_INVALID, "envcfg belongs to another network");
+    if (int rc = validate_actions(b, actions, A, offset)) return rc;
+    size_t ab = 4 * (size_t)A * b->B;
+    if (int rc = b->s_act.ensure(ab)) return rc;
+    if (int rc = b->s_obs.ensure(8 * (size_t)b->W * b->B)) return rc;
+    if (int rc = b->s_rew.ensure(4 * b->B)) return rc;
+    if (int rc = b->s_flags.ensure(b->B)) return rc;
+    if (int rc = b->s_nup.ensure(4 * b->B)) return rc;
+    HIP_TRY(hipMemcpyAsync(b->s_act.p, actions, ab, hipMemcpyHostToDevice, b->stream));
+    return 0;
+}
+
+static int env_host_out(pbn_batch* b, uint64_t* obs, int32_t* reward, uint8_t* flags, uint32_t* n_updates) {
+    if (obs) HIP_TRY(hipMemcpyAsync(obs, b->s_obs.p, 8 * (size_t)b->W * b->B, hipMemcpyDeviceToHost, b->stream));
+    if (reward) HIP_TRY(hipMemcpyAsync(reward, b->s_rew.p, 4 * b->B, hipMemcpyDeviceToHost, b->stream));
+    if (flags) HIP_TRY(hipMemcpyAsync(flags, b->s_flags.p, b->B, hipMemcpyDeviceToHost, b->stream));
+    if (n_updates) HIP_TRY(hipMemcpyAsync(n_updates, b->s_nup.p, 4 * b->B, hipMemcpyDeviceToHost, b->stream));
+    int32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, b->d_error, 4, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    if (err) return fail(PBN_E_RANGE, "an action was out of range");
+    return 0;
+}
+
+int pbn_env_step_multi(pbn_batch* b, const pbn_envcfg* cfg_c, const int32_t* actions, int A, int dedup, int offset,
+                       uint32_t update_cap, uint64_t* obs, int32_t* reward, uint8_t* flags, uint32_t* n_updates) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(cfg_c, "cfg");
+    CHECK_NN(actions, "actions");
+    pbn_envcfg* cfg = const_cast<pbn_envcfg*>(cfg_c);
+    SET_DEV(b);
+    if (int rc = env_host_common(b, cfg, actions, A, offset)) return rc;
+    if (int rc = env_launch(b, cfg, (const int32_t*)b->s_act.p, A, dedup, offset, update_cap, (uint64_t*)b->s_obs.p,
+                            (int32_t*)b->s_rew.p, (uint8_t*)b->s_flags.p, (uint32_t*)b->s_nup.p, 0, nullptr, nullptr,
+                            nullptr))
+        return rc;
+    return env_host_out(b, obs, reward, flags, n_updates);
+}
+
+int pbn_env_step_multi_device(pbn_batch* b, const pbn_envcfg* cfg_c, const int32_t* d_actions, int A, int dedup,
+                              int offset, uint32_t update_cap, uint64_t* d_obs, int32_t* d_reward, uint8_t* d_flags,
+                              uint32_t* d_n_updates) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(cfg_c, "cfg");
+    CHECK_NN(d_actions, "d_actions");
+    CHECK_NN(d_obs, "d_obs");
+    CHECK_NN(d_reward, "d_reward");
+    CHECK_NN(d_flags, "d_flags");
+    CHECK_NN(d_n_updates, "d_n_updates");
+    pbn_envcfg* cfg = const_cast<pbn_envcfg*>(cfg_c);
+    if (cfg->net != b->net) return fail(PBN_E_INVALID, "envcfg belongs to another network");
+    if (A < 1 || A > 4096) return fail(PBN_E_INVALID, "A=%d outside [1, 4096]", A);
+    if (offset != 0 && offset != 1) return fail(PBN_E_INVALID, "offset must be 0 or 1");
+    SET_DEV(b);
+    return env_launch(b, cfg, d_actions, A, dedup, offset, update_cap, d_obs, d_reward, d_flags, d_n_updates, 0,
+                      nullptr, nullptr, nullptr);
+}
+
+int pbn_env_step_multi_replay(pbn_batch* b, const pbn_envcfg* cfg_c, const int32_t* actions, int A, int dedup,
+                              int offset, const int64_t* draw_offsets, const uint32_t* draws_i,
+                              const uint64_t* draws_k, uint64_t* obs, int32_t* reward, uint8_t* flags,
+                              uint32_t* n_updates) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(cfg_c, "cfg");
+    CHECK_NN(actions, "actions");
+    CHECK_NN(draw_offsets, "draw_offsets");
+    pbn_envcfg* cfg = const_cast<pbn_envcfg*>(cfg_c);
+    const int64_t nd = draw_offsets[b->B];
+    if (draw_offsets[0] != 0 || nd < 0) return fail(PBN_E_INVALID, "draw_offsets must start at 0");
+    for (uint64_t e = 0; e < b->B; e++)
+        if (draw_offsets[e + 1] < draw_offsets[e]) return fail(PBN_E_INVALID, "draw_offsets not non-decreasing");
+    const uint32_t lo = b->net->kind == PBN_KIND_PROB_TABLE ? 1u : 0u;
+    for (int64_t q = 0; q < nd; q++)
+        if (draws_i[q] >= (uint32_t)b->N || draws_i[q] < lo || (draws_k[q] >> 53))
+            return fail(PBN_E_RANGE, "replay draw %lld out of range", (long long)q);
+    SET_DEV(b);
+    if (int rc = env_host_common(b, cfg, actions, A, offset)) return rc;
+    if (int rc = b->s_off.ensure(8 * (b->B + 1))) return rc;
+    if (int rc = b->s_replay_i.ensure(4 * (size_t)std::max<int64_t>(nd, 1))) return rc;
+    if (int rc = b->s_replay_k.ensure(8 * (size_t)std::max<int64_t>(nd, 1))) return rc;
+    HIP_TRY(hipMemcpyAsync(b->s_off.p, draw_offsets, 8 * (b->B + 1), hipMemcpyHostToDevice, b->stream));
+    if (nd) {
+        HIP_TRY(hipMemcpyAsync(b->s_replay_i.p, draws_i, 4 * (size_t)nd, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(b->s_replay_k.p, draws_k, 8 * (size_t)nd, hipMemcpyHostToDevice, b->stream));
+    }
+    if (int rc = env_launch(b, cfg, (const int32_t*)b->s_act.p, A, dedup, offset, 0xFFFFFFFFu, (uint64_t*)b->s_obs.p,
+                            (int32_t*)b->s_rew.p, (uint8_t*)b->s_flags.p, (uint32_t*)b->s_nup.p, 1, b->s_off.p,
+                            b->s_replay_i.p, b->s_replay_k.p))
+        return rc;
+    return env_host_out(b, obs, reward, flags, n_updates);
+}
+
+// ------------------------------------------------------------------ timing
+int pbn_timing_enable(pbn_batch* b, int enable) {
+    CHECK_NN(b, "batch");
+    b->timing = enable != 0;
+    b->ev_used = 0;
+    return 0;
+}
+
+int pbn_timing_read(pbn_batch* b, double* kernel_ms, uint64_t* launches) {
+    CHECK_NN(b, "batch");
+    SET_DEV(b);
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    double tot = 0;
+    for (size_t k = 0; k < b->ev_used; k++) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev_pool[k].first, b->ev_pool[k].second));
+        tot += ms;
+    }
+    if (kernel_ms) *kernel_ms = tot;
+    if (launches) *launches = b->ev_used;
+    b->ev_used = 0;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+// pbn_device.hpp -- device-side building blocks of the gfx950 PBN kernels.
+//
+// One lane owns one env: its W = ceil(N/64) state words live in VGPRs for the
+// whole launch; the network tables live in LDS (staged once per workgroup from
+// a packed "image" built on the host, see pbn_abi.cpp: build_image()).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pbn_params.hpp"
+
+namespace pbn {
+
+// ---------------------------------------------------------------- Philox4x32-10
+// Random123's Philox4x32 with 10 rounds (KAT-checked in tests/test_oracle.py and
+// tests/test_gpu_parity.py). Each round is two 32x32->64 multiplies
+// (v_mad_u64_u32) and four XORs.
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1;
+        c[3] = (uint32_t)p0;
+        c[0] = n0;
+        c[2] = n2;
+    }
+}
+
+// Counter layout (shared with oracle/pbn_oracle.c philox_draw):
+//   ctr = {c0, c1, gid_lo, (gid_hi & 0xFFFFFF) | stream << 24}, key = {seed_lo, seed_hi}
+__device__ __forceinline__ void philox_draw(uint64_t seed, uint32_t c0, uint32_t c1, uint64_t gid, uint32_t stream,
+                                            uint32_t w[4]) {
+    w[0] = c0;
+    w[1] = c1;
+    w[2] = (uint32_t)gid;
+    w[3] = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (stream << 24);
+    philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// random() == k53 * 2^-53, built CPython-style from two words (a>>5, b>>6).
+__device__ __forceinline__ uint64_t k53_of(uint32_t a, uint32_t b) {
+    return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+}
+
+// ---------------------------------------------------------------- packed state
+// The state words must stay in VGPRs: a select chain over s[k] is recognised by
+// the compiler as s[i >> 6] and demoted to a scratch array, so word selection is
+// written as bitwise masks over 32-bit halves (no indexing).
+__device__ __forceinline__ uint32_t lane_mask(uint32_t a, uint32_t b) { return 0u - (uint32_t)(a == b); }
+
+template <int W>
+__device__ __forceinline__ uint32_t getbit(const uint64_t (&s)[W], uint32_t i) {
+    const uint32_t wi = i >> 6, sh = i & 31u, hi = (i >> 5) & 1u;
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const uint32_t m = lane_mask(wi, (uint32_t)k);
+        x |= ((uint32_t)(s[k] >> 32) & m & (0u - hi)) | ((uint32_t)s[k] & m & (hi - 1u));
+    }
+    return (x >> sh) & 1u;
+}
+
+template <int W>
+__device__ __forceinline__ void setbit(uint64_t (&s)[W], uint32_t i, uint32_t v) {
+    const uint64_t bit = (uint64_t)1 << (i & 63u);
+    const uint64_t val = (uint64_t)(v & 1u) << (i & 63u);
+    const uint32_t wi = i >> 6;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const uint64_t m = (uint64_t)(int64_t)(int32_t)lane_mask(wi, (uint32_t)k);
+        s[k] = (s[k] & ~(bit & m)) | (val & m);
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void load_state(const uint64_t* __restrict__ p, uint64_t (&s)[W]) {
+    if constexpr (W % 2 == 0) {
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
+#pragma unroll
+        for (int k = 0; k < W / 2; ++k) {
+            ulonglong2 v = q[k];
+            s[2 * k] = v.x;
+            s[2 * k + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < W; ++k) s[k] = p[k];
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void store_state(uint64_t* __restrict__ p, const uint64_t (&s)[W]) {
+    if constexpr (W % 2 == 0) {
+        ulonglong2* q = reinterpret_cast<ulonglong2*>(p);
+#pragma unroll
+        for (int k = 0; k < W / 2; ++k) q[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < W; ++k) p[k] = s[k];
+    }
+}
+
+// Store only the 16-byte pairs (8-byte words for odd W) whose dirty bit is set.
+template <int W>
+__device__ __forceinline__ void store_dirty(uint64_t* __restrict__ p, const uint64_t (&s)[W], uint32_t dirty) {
+    if constexpr (W % 2 == 0) {
+        ulonglong2* q = reinterpret_cast<ulonglong2*>(p);
+#pragma unroll
+        for (int k = 0; k < W / 2; ++k)
+            if (dirty & (3u << (2 * k))) q[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+            if (dirty & (1u << k)) p[k] = s[k];
+    }
+}
+
+// ---------------------------------------------------------------- LDS staging
+// Copy the network image (16-byte granules) into LDS; every thread participates.
+__device__ __forceinline__ void stage_image(const uint4* __restrict__ img, uint32_t n16, uint4* lds) {
+    for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) lds[k] = img[k];
+}
+
+// ---------------------------------------------------------------- node updates
+// Bittner Predstep (base.py:89-119) in integer form.
+//   node_info[i] = first predictor (low 16) | predictor count (high 16)
+//   thr[j]      = 53-bit selection threshold, rec[j] = in0 | in1<<16 | in2<<32 | tt<<48
+template <int W>
+__device__ __forceinline__ uint32_t predictor_update(uint64_t (&s)[W], uint32_t i, uint64_t k53, const uint8_t* lds,
+                                                     const NetLayout& L) {
+    const uint32_t info = reinterpret_cast<const uint32_t*>(lds + L.off_node)[i];
+    const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
+    const uint64_t* thr = reinterpret_cast<const uint64_t*>(lds + L.off_thr);
+    uint32_t j = o0;
+    for (uint32_t q = 1; q < cnt; ++q) j += (k53 >= thr[o0 + q - 1]) ? 1u : 0u;
+    const uint64_t rec = reinterpret_cast<const uint64_t*>(lds + L.off_rec)[j];
+    const uint32_t p = (getbit<W>(s, (uint32_t)rec & 0xFFFFu) << 3) |
+                       (getbit<W>(s, (uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
+                       (getbit<W>(s, (uint32_t)(rec >> 32) & 0xFFFFu) << 1) | getbit<W>(s, i);
+    const uint32_t y = (uint32_t)(rec >> (48 + p)) & 1u;
+    setbit<W>(s, i, y);
+    return y;
+}
+
+// PBN node update (common/node.py:31-38): k53 < ceil(p * 2^53), table index in C order.
+//   node_info[i] = thr offset (low 32) | input offset (bits 32..47) | k (bits 48..55)
+template <int W>
+__device__ __forceinline__ uint32_t table_update(uint64_t (&s)[W], uint32_t i, uint64_t k53, const uint8_t* lds,
+                                                 const NetLayout& L) {
+    const uint64_t info = reinterpret_cast<const uint64_t*>(lds + L.off_node)[i];
+    const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu, k = (uint32_t)(info >> 48) & 0xFFu;
+    const uint16_t* in = reinterpret_cast<const uint16_t*>(lds + L.off_rec) + ioff;
+    uint32_t idx = 0;
+    for (uint32_t q = 0; q < k; ++q) idx = (idx << 1) | getbit<W>(s, in[q]);
+    const uint64_t t = reinterpret_cast<const uint64_t*>(lds + L.off_thr)[toff + idx];
+    const uint32_t y = k53 < t ? 1u : 0u;
+    setbit<W>(s, i, y);
+    return y;
+}
+
+template <int W, int KIND>
+__device__ __forceinline__ uint32_t node_update(uint64_t (&s)[W], uint32_t i, uint64_t k53, const uint8_t* lds,
+                                                const NetLayout& L) {
+    if constexpr (KIND == KIND_PREDICTOR_MIX)
+        return predictor_update<W>(s, i, k53, lds, L);
+    else
+        return table_update<W>(s, i, k53, lds, L);
+}
+
+// Philox (node, k53) for update counter c0/c1 of env gid.
+//   Bittner: node in [0, N-1] (base.py:308); PBN: node in [1, N-1] (pbn.py:131).
+template <int KIND>
+__device__ __forceinline__ uint32_t philox_node(uint32_t w0, uint32_t N) {
+    if constexpr (KIND == KIND_PREDICTOR_MIX)
+        return __umulhi(w0, N);
+    else
+        return 1u + __umulhi(w0, N - 1u);
+}
+
+}  // namespace pbn

@@ -1,0 +1,348 @@
+// pbn_kernels.hip -- gfx950 kernels of the vectorised PBN simulator.
+//
+// Mapping: one lane = one env (state in VGPRs), one 256-thread workgroup stages
+// the network image (node info, 53-bit selection thresholds, predictor records
+// or probability thresholds) into LDS once, then walks envs in a grid-stride loop.
+// The grid is sized to what is resident (CUs x blocks/CU), so the LDS staging is
+// paid once per resident workgroup, not once per 256 envs.
+//
+// Reference semantics implemented (file:line in the reference):
+//   k_step    Graph.step base.py:306-312 (+ Node.Predstep :89-119) and
+//             PBN.step common/pbn.py:129-133 (+ Node.compute_next_value common/node.py:34-38)
+//   k_init    Graph.genRandState base.py:368-370 / PBN.reset(None) pbn.py:105-118 /
+//             PBNTargetMultiEnv.reset pbn_target_multi.py:237-249 (Philox streams)
+//   k_flip    Graph.flipNode base.py:280-284 over a multi-action row (pbn_target_multi.py:120-131)
+//   k_env     PBNTargetMultiEnv.step pbn_target_multi.py:119-154
+#include <hip/hip_runtime.h>
+
+#include "pbn_device.hpp"
+#include "pbn_params.hpp"
+
+namespace pbn {
+
+// ------------------------------------------------------------------ step
+template <int W, int KIND, int STORE, int REPLAY>
+__global__ __launch_bounds__(BLOCK) void k_step(StepArgs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    __syncthreads();
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < a.B; e += stride) {
+        uint64_t s[W];
+        load_state<W>(a.state + e * W, s);
+        uint32_t dirty = 0;
+        const uint64_t g = a.env_base + e;
+        for (uint32_t t = 0; t < a.T; ++t) {
+            uint32_t i;
+            uint64_t k53;
+            if constexpr (REPLAY) {
+                i = a.replay_node[(uint64_t)t * a.B + e];
+                k53 = a.replay_k53[(uint64_t)t * a.B + e];
+            } else {
+                const uint64_t u = a.update_base + t;
+                uint32_t w[4];
+                philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
+                i = philox_node<KIND>(w[0], N);
+                k53 = k53_of(w[1], w[2]);
+            }
+            const uint32_t old = getbit<W>(s, i);
+            const uint32_t y = node_update<W, KIND>(s, i, k53, lds, a.L);
+            dirty |= (old != y ? 1u : 0u) << (i >> 6);
+        }
+        if constexpr (STORE == STORE_DIRTY)
+            store_dirty<W>(a.state + e * W, s, dirty);
+        else
+            store_state<W>(a.state + e * W, s);
+    }
+}
+
+// ------------------------------------------------------------------ init / reset
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_init(InitArgs a) {
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= a.B) return;
+    if (a.mask && !a.mask[e]) return;
+    const uint64_t g = a.env_base + e;
+    uint64_t s[W];
+#pragma unroll
+    for (int m = 0; 2 * m < W; ++m) {
+        uint32_t w[4];
+        philox_draw(a.seed, (uint32_t)m + (a.cube_care ? 1u : 0u), a.reset_count, g,
+                    a.cube_care ? STREAM_RESET : STREAM_INIT, w);
+        s[2 * m] = ((uint64_t)w[1] << 32) | w[0];
+        if (2 * m + 1 < W) s[2 * m + 1] = ((uint64_t)w[3] << 32) | w[2];
+    }
+    if (a.cube_care) {
+        uint32_t w[4];
+        philox_draw(a.seed, 0u, a.reset_count, g, STREAM_RESET, w);
+        const uint32_t c = __umulhi(w[0], (uint32_t)a.n_cubes);
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const uint64_t care = a.cube_care[(uint64_t)c * W + k];
+            s[k] = (a.cube_value[(uint64_t)c * W + k] & care) | (s[k] & ~care);
+        }
+    }
+    const int r = a.n_nodes & 63;
+    if (r) s[W - 1] &= (((uint64_t)1 << r) - 1);
+    if (a.kind == KIND_PROB_TABLE) s[0] &= ~(uint64_t)1;  // pbn.py:118 state[0] = 0
+    store_state<W>(a.state + e * W, s);
+    if (a.n_steps) a.n_steps[e] = 0;
+}
+
+// Python list indexing of flipNode(a - offset): valid for -N <= idx < N.
+__device__ __forceinline__ bool action_node(int32_t a, int32_t offset, int32_t N, uint32_t* node) {
+    const int32_t idx = a - offset;
+    if (idx >= N || idx < -N) return false;
+    *node = (uint32_t)(idx < 0 ? idx + N : idx);
+    return true;
+}
+
+// Flip every (unique, if dedup) non-zero action of the row; returns the number of
+// actions counted by the reference's reward (unique values incl. 0, or A).
+template <int W>
+__device__ __forceinline__ int apply_actions(uint64_t (&s)[W], const int32_t* row, int32_t A, int32_t offset,
+                                             int32_t dedup, int32_t N, bool* bad) {
+    int n_act = 0;
+    for (int32_t k = 0; k < A; ++k) {
+        const int32_t v = row[k];
+        bool dup = false;
+        if (dedup)
+            for (int32_t q = 0; q < k; ++q) dup |= (row[q] == v);
+        if (dup) continue;
+        ++n_act;
+        if (v == 0) continue;
+        uint32_t node;
+        if (!action_node(v, offset, N, &node)) {
+            *bad = true;
+            continue;
+        }
+        setbit<W>(s, node, getbit<W>(s, node) ^ 1u);
+    }
+    return dedup ? n_act : A;
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_flip(FlipArgs a) {
+    const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= a.B) return;
+    uint64_t s[W];
+    load_state<W>(a.state + e * W, s);
+    bool bad = false;
+    apply_actions<W>(s, a.actions + e * (uint64_t)a.A, a.A, a.offset, a.dedup, a.n_nodes, &bad);
+    if (bad) {
+        atomicOr(a.error, 1);
+        return;  // leave this env untouched
+    }
+    store_state<W>(a.state + e * W, s);
+}
+
+// ------------------------------------------------------------------ R6 env step
+template <int W>
+__device__ __forceinline__ bool cube_match(const uint64_t (&s)[W], const uint64_t* cv) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < W; ++k) ok &= ((s[k] & cv[k]) == cv[W + k]);
+    return ok;
+}
+
+template <int W>
+__device__ __forceinline__ bool attracting(const uint64_t (&s)[W], const uint64_t* cubes, int32_t H) {
+    bool hit = false;
+    for (int32_t h = 0; h < H && !hit; ++h) hit = cube_match<W>(s, cubes + (uint64_t)h * 2 * W);
+    return hit;
+}
+
+template <int W, int KIND, int REPLAY>
+__global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    __syncthreads();
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
+    const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < a.B; e += stride) {
+        uint64_t s[W];
+        load_state<W>(a.state + e * W, s);
+        const int64_t nst = a.n_steps[e] + 1;  // :123
+        bool bad = false;
+        uint64_t s_in[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) s_in[k] = s[k];
+        const int n_act = apply_actions<W>(s, a.actions + e * (uint64_t)a.A, a.A, a.offset, a.dedup, (int32_t)N, &bad);
+        if (bad) {  // reference raises ValueError; this env is left untouched
+            atomicOr(a.error, 1);
+            continue;
+        }
+        uint64_t o[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) o[k] = s[k];  // :133 observation before the update
+        (void)s_in;
+        const uint64_t g = a.env_base + e;
+        uint32_t used = 0;
+        bool capped = false;
+        int64_t dpos = 0, dend = 0;
+        if constexpr (REPLAY) {
+            dpos = a.draw_off[e];
+            dend = a.draw_off[e + 1];
+        }
+        for (;;) {
+            if (used >= a.update_cap) {
+                capped = true;
+                break;
+            }
+            uint32_t i;
+            uint64_t k53;
+            if constexpr (REPLAY) {
+                if (dpos >= dend) {
+                    capped = true;
+                    break;
+                }
+                i = a.draws_i[dpos];
+                k53 = a.draws_k[dpos];
+                ++dpos;
+            } else {
+                uint32_t w[4];
+                philox_draw(a.seed, used, a.call_idx, g, STREAM_ENV, w);
+                i = philox_node<KIND>(w[0], N);
+                k53 = k53_of(w[1], w[2]);
+            }
+            node_update<W, KIND>(s, i, k53, lds, a.L);
+            ++used;
+            // :134 the first update's result is discarded; :135-146 loop until attracting
+            if (used > 1) {
+#pragma unroll
+                for (int k = 0; k < W; ++k) o[k] = s[k];
+            }
+            if (attracting<W>(o, cubes, a.n_cubes)) break;
+        }
+        store_state<W>(a.state + e * W, s);
+        store_state<W>(a.obs + e * W, o);
+        a.n_steps[e] = nst;
+        const bool term = cube_match<W>(o, target);  // :190-199 (target[0] only)
+        a.reward[e] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
+        a.flags[e] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
+        a.n_updates[e] = used;
+    }
+}
+
+// ------------------------------------------------------------------ dispatch
+template <int W, int KIND>
+static void* step_fn(int store, int replay) {
+    if (replay) return (void*)k_step<W, KIND, STORE_FULL, 1>;
+    return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0> : (void*)k_step<W, KIND, STORE_FULL, 0>;
+}
+
+template <int KIND>
+static void* step_fn_w(int W, int store, int replay) {
+    switch (W) {
+        case 1: return step_fn<1, KIND>(store, replay);
+        case 2: return step_fn<2, KIND>(store, replay);
+        case 3: return step_fn<3, KIND>(store, replay);
+        case 4: return step_fn<4, KIND>(store, replay);
+        case 5: return step_fn<5, KIND>(store, replay);
+        case 6: return step_fn<6, KIND>(store, replay);
+        case 7: return step_fn<7, KIND>(store, replay);
+        case 8: return step_fn<8, KIND>(store, replay);
+    }
+    return nullptr;
+}
+
+template <int KIND>
+static void* env_fn_w(int W, int replay) {
+#define PBN_ENV_CASE(w) \
+    case w: return replay ? (void*)k_env<w, KIND, 1> : (void*)k_env<w, KIND, 0>;
+    switch (W) {
+        PBN_ENV_CASE(1)
+        PBN_ENV_CASE(2)
+        PBN_ENV_CASE(3)
+        PBN_ENV_CASE(4)
+        PBN_ENV_CASE(5)
+        PBN_ENV_CASE(6)
+        PBN_ENV_CASE(7)
+        PBN_ENV_CASE(8)
+    }
+#undef PBN_ENV_CASE
+    return nullptr;
+}
+
+static void* init_fn(int W) {
+    switch (W) {
+        case 1: return (void*)k_init<1>;
+        case 2: return (void*)k_init<2>;
+        case 3: return (void*)k_init<3>;
+        case 4: return (void*)k_init<4>;
+        case 5: return (void*)k_init<5>;
+        case 6: return (void*)k_init<6>;
+        case 7: return (void*)k_init<7>;
+        case 8: return (void*)k_init<8>;
+    }
+    return nullptr;
+}
+
+static void* flip_fn(int W) {
+    switch (W) {
+        case 1: return (void*)k_flip<1>;
+        case 2: return (void*)k_flip<2>;
+        case 3: return (void*)k_flip<3>;
+        case 4: return (void*)k_flip<4>;
+        case 5: return (void*)k_flip<5>;
+        case 6: return (void*)k_flip<6>;
+        case 7: return (void*)k_flip<7>;
+        case 8: return (void*)k_flip<8>;
+    }
+    return nullptr;
+}
+
+static int launch(void* fn, int grid, uint32_t lds, void* stream, void* args, size_t args_size) {
+    if (!fn) return (int)hipErrorInvalidValue;
+    (void)args_size;
+    void* kargs[] = {args};
+    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
+}
+
+int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream) {
+    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay)
+                                              : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay);
+    StepArgs c = a;
+    return launch(fn, grid, a.L.bytes, stream, &c, sizeof c);
+}
+
+int launch_init(int W, const InitArgs& a, int grid, void* stream) {
+    InitArgs c = a;
+    return launch(init_fn(W), grid, 0, stream, &c, sizeof c);
+}
+
+int launch_flip(int W, const FlipArgs& a, int grid, void* stream) {
+    FlipArgs c = a;
+    return launch(flip_fn(W), grid, 0, stream, &c, sizeof c);
+}
+
+int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream) {
+    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay)
+                                              : env_fn_w<KIND_PROB_TABLE>(W, replay);
+    EnvArgs c = a;
+    return launch(fn, grid, a.L.bytes, stream, &c, sizeof c);
+}
+
+static int occupancy(void* fn, uint32_t lds, int* blocks_per_cu) {
+    int nb = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, BLOCK, lds);
+    if (e != hipSuccess) return (int)e;
+    *blocks_per_cu = nb < 1 ? 1 : nb;
+    return 0;
+}
+
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
+    void* fn = kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, STORE_FULL, 0)
+                                          : step_fn_w<KIND_PROB_TABLE>(W, STORE_FULL, 0);
+    return occupancy(fn, lds_bytes, blocks_per_cu);
+}
+
+int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
+    void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0) : env_fn_w<KIND_PROB_TABLE>(W, 0);
+    return occupancy(fn, lds_bytes, blocks_per_cu);
+}
+
+}  // namespace pbn

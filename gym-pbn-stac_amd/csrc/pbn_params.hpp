@@ -1,0 +1,89 @@
+// pbn_params.hpp -- plain structs shared by the host ABI (g++) and the kernels (hipcc).
+#pragma once
+#include <stdint.h>
+
+namespace pbn {
+
+enum { KIND_PREDICTOR_MIX = 1, KIND_PROB_TABLE = 2 };
+enum { STREAM_STEP = 1, STREAM_INIT = 2, STREAM_ENV = 3, STREAM_RESET = 4 };
+enum { STORE_FULL = 0, STORE_DIRTY = 1 };
+
+constexpr int BLOCK = 256;          // 4 wave64 per workgroup
+constexpr int MAX_WORDS = 8;        // N <= 512
+constexpr uint32_t MAX_IMAGE = 64 * 1024;  // LDS bytes for the network image
+
+// Byte offsets of the tables inside the LDS image (16-byte aligned image).
+struct NetLayout {
+    uint32_t off_node;  // per-node info
+    uint32_t off_thr;   // u64 thresholds
+    uint32_t off_rec;   // predictor records (u64) or input lists (u16)
+    uint32_t bytes;     // total, multiple of 16
+    int32_t kind;
+    int32_t n_nodes;
+};
+
+struct StepArgs {
+    uint64_t* state;             // [B][W]
+    const void* img;             // network image (device, 16-B aligned)
+    NetLayout L;
+    uint64_t B;
+    uint64_t env_base;           // global id of env 0 of this batch
+    uint64_t seed;
+    uint64_t update_base;        // Philox update counter of the first update
+    uint32_t T;                  // updates per launch
+    const uint32_t* replay_node; // [T][B] (replay mode)
+    const uint64_t* replay_k53;  // [T][B]
+};
+
+struct InitArgs {
+    uint64_t* state;
+    uint64_t B, env_base, seed;
+    uint32_t reset_count;
+    int32_t n_nodes, kind;
+    // env reset (R6): choose a cube among n_cubes, keep its cared bits, draw the rest
+    const uint64_t* cube_care;   // [n_cubes][W] or null (plain randomize)
+    const uint64_t* cube_value;
+    int32_t n_cubes;
+    const uint8_t* mask;         // [B] or null
+    int64_t* n_steps;            // zeroed for reset envs, if non-null
+};
+
+struct FlipArgs {
+    uint64_t* state;
+    const int32_t* actions;  // [B][A]
+    uint64_t B;
+    int32_t A, offset, dedup, n_nodes;
+    int32_t* error;          // set to 1 on an out-of-range action (device path)
+};
+
+struct EnvArgs {
+    uint64_t* state;         // [B][W]
+    int64_t* n_steps;        // [B]
+    const int32_t* actions;  // [B][A]
+    uint64_t* obs;           // [B][W]
+    int32_t* reward;         // [B]
+    uint8_t* flags;          // [B]
+    uint32_t* n_updates;     // [B]
+    int32_t* error;
+    const void* img;         // network image + cubes appended
+    NetLayout L;
+    uint32_t off_cubes;      // care/value pairs [H][2][W] u64 inside the LDS image
+    uint32_t off_target;     // target care/value [2][W]
+    int32_t n_cubes;
+    uint64_t B, env_base, seed;
+    uint32_t call_idx, update_cap;
+    int32_t A, offset, dedup, horizon, reward_success, action_cost;
+    const int64_t* draw_off;  // replay mode: [B+1]
+    const uint32_t* draws_i;
+    const uint64_t* draws_k;
+};
+
+// Launchers (pbn_kernels.hip). Return hipError_t as int.
+int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream);
+int launch_init(int W, const InitArgs& a, int grid, void* stream);
+int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
+int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
+int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
+
+}  // namespace pbn

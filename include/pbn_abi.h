@@ -1,0 +1,180 @@
+/*
+ * pbn_abi.h -- C ABI of libpbnsim.so, the MI355X (gfx950) vectorised PBN simulator.
+ *
+ * The reference (jakub-zarzycki2022/gym-PBN-stac) is pure Python; its hot path
+ * sits behind plain method calls. Each entry point below names the reference
+ * interface it replaces (file:line, relative to the reference root). A Python
+ * ctypes binding lives in gym-pbn-stac_amd/gym_pbn_amd/_lib.py; INTEGRATION.md
+ * shows the binding a gym-PBN maintainer would add.
+ *
+ * Conventions
+ *  - Every function returns PBN_OK (0) or a negative PBN_E_* code and never
+ *    aborts; pbn_last_error() returns a thread-local message for the last failure.
+ *  - State is bit-packed: env e, node i lives in bit (i % 64) of word
+ *    e*W + i/64, W = ceil(N/64). Host arrays are [B][W] uint64.
+ *  - The library owns all device memory and copies network tables; callers own
+ *    host arrays, which are read or written only during the call.
+ *  - One batch = one device + one HIP stream. Calls on one batch must be
+ *    serialised by the caller; different batches may be driven from different
+ *    threads. Functions taking host outputs synchronise the batch stream; the
+ *    rest are asynchronous until pbn_sync().
+ *  - RNG modes: PHILOX (production; counter-based, keyed by
+ *    (seed, global env id, update counter) so results do not depend on batch
+ *    size or GPU count), REPLAY (caller supplies the reference's own draws), and
+ *    MT (each env runs CPython's MT19937 -- and for probability-table networks
+ *    numpy's legacy MT19937 too -- seeded like random.seed(s)/np.random.seed(s),
+ *    reproducing the reference trajectory from the seed alone).
+ */
+#ifndef PBN_ABI_H
+#define PBN_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBN_ABI_VERSION 1
+
+enum {
+    PBN_OK = 0,
+    PBN_E_INVALID = -1,     /* bad argument / descriptor */
+    PBN_E_RANGE = -2,       /* node or action out of range (reference: ValueError, base.py:283-284) */
+    PBN_E_HIP = -3,         /* HIP runtime failure */
+    PBN_E_NOMEM = -4,       /* device allocation failed */
+    PBN_E_UNSUPPORTED = -5, /* network outside kernel limits (N > 512, tables > LDS budget) */
+    PBN_E_STATE = -6        /* wrong mode / uninitialised (reference: Exception, base.py:90-91) */
+};
+
+enum { PBN_KIND_PREDICTOR_MIX = 1, PBN_KIND_PROB_TABLE = 2 };
+
+typedef struct pbn_net pbn_net;
+typedef struct pbn_batch pbn_batch;
+typedef struct pbn_envcfg pbn_envcfg;
+
+/* Network tables (see gym_pbn_amd/network.py for how they are derived).
+ * PREDICTOR_MIX replaces base.Node.predictors (base.py:30-45) + Predstep (:89-119):
+ *   pred_offsets [N+1], pred_inputs [P][3] node indices, pred_tt [P] 16-entry truth
+ *   table over (x0<<3|x1<<2|x2<<1|x_self), pred_thr [P] exact 53-bit selection
+ *   thresholds (predictor j is selected for the first j with k53 < thr[j]).
+ * PROB_TABLE replaces common/node.py Node (input_mask, function; :22-38):
+ *   node_k [N], input_offsets [N+1], inputs [sum k] (ascending, first = MSB),
+ *   thr_offsets [N+1], thr [sum 2^k] = ceil(p * 2^53). */
+typedef struct {
+    int32_t kind;
+    int32_t n_nodes;
+    int32_t n_preds;
+    const int32_t *pred_offsets;
+    const int32_t *pred_inputs;
+    const uint16_t *pred_tt;
+    const uint64_t *pred_thr;
+    const int32_t *node_k;
+    const int32_t *input_offsets;
+    const int32_t *inputs;
+    const int64_t *thr_offsets;
+    const uint64_t *thr;
+} pbn_net_desc;
+
+typedef struct {
+    int32_t n_nodes, n_words, kind, device;
+    uint64_t n_envs, env_id_base, seed;
+    uint64_t update_count; /* Philox updates applied so far (batch-wide counter) */
+    uint32_t env_call_count, reset_count;
+    int32_t mt_ready; /* 1 after pbn_mt_seed */
+} pbn_batch_info;
+
+/* Attractor / goal description for the multi-flip env step (R6).
+ * cubes: union of the attractor hypercubes (cabean output, '*' = don't care),
+ *   care/value [n_cubes][W]: state s is attracting iff (s & care) == value for
+ *   some cube -- the membership test of the expanded set built at
+ *   pbn_target_multi.py:437-455 and queried at :489-492.
+ * reset cubes: all_attractors[0] (reset draws one and fills '*' bits, :237-249).
+ * target: all_attractors[-1][0] -- in_target() only ever tests target[0] (:190-199). */
+typedef struct {
+    int32_t n_cubes;
+    const uint64_t *cube_care;
+    const uint64_t *cube_value;
+    int32_t n_reset_cubes;
+    const uint64_t *reset_care;
+    const uint64_t *reset_value;
+    const uint64_t *target_care;  /* [W] */
+    const uint64_t *target_value; /* [W] */
+    int32_t horizon;              /* truncated = n_steps == horizon (:224) */
+    int32_t reward_success;       /* +1000 (:218-219) */
+    int32_t action_cost;          /* 1 per unique action value (:222) */
+} pbn_envcfg_desc;
+
+/* flags returned per env by pbn_env_step_multi* */
+enum { PBN_FLAG_TERMINATED = 1, PBN_FLAG_TRUNCATED = 2, PBN_FLAG_CAPPED = 4 };
+
+/* ---- library ---- */
+int pbn_abi_version(void);
+const char *pbn_last_error(void);
+int pbn_device_count(int *count);
+
+/* ---- networks: replaces graph construction, bittner/utils.py:81-91 / pbn.py:78-87 ---- */
+int pbn_net_create(const pbn_net_desc *desc, pbn_net **out);
+void pbn_net_destroy(pbn_net *net);
+
+/* ---- batches of independent envs (the reference holds one Graph per env) ---- */
+int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
+                     pbn_batch **out);
+void pbn_batch_destroy(pbn_batch *b);
+int pbn_batch_get_info(const pbn_batch *b, pbn_batch_info *info);
+int pbn_sync(pbn_batch *b);
+
+/* ---- state I/O: Graph.setState / getState (base.py:364-366, 320-324), PBN.reset(state) (pbn.py:96-119) ---- */
+int pbn_set_state(pbn_batch *b, const uint64_t *words);          /* host [B][W] */
+int pbn_get_state(pbn_batch *b, uint64_t *words);                /* host [B][W] */
+int pbn_set_state_device(pbn_batch *b, const void *dev_words);   /* device [B][W], same device */
+int pbn_get_state_device(pbn_batch *b, void *dev_words);
+/* Graph.genRandState (base.py:368-370) / PBN.reset(None) (pbn.py:105-118) in Philox mode */
+int pbn_randomize_state(pbn_batch *b);
+
+/* ---- intervention: Graph.flipNode (base.py:280-284), PBN.flip (pbn.py:121-127) ----
+ * actions [B][A] host int32; value 0 = no action, value v flips node v - offset
+ * (offset 1: gym-PBN target envs, pbn_target.py:266-267; offset 0: PBNEnv, pbn_env.py:141-142).
+ * dedup 1: act on unique values per row (torch-tensor input, pbn_target_multi.py:120-121). */
+int pbn_flip(pbn_batch *b, const int32_t *actions, int A, int offset, int dedup);
+
+/* ---- the hot path: Graph.step (base.py:306-312) / PBN.step (pbn.py:129-133) ---- */
+/* Philox mode, n_updates launches of one update each (state round-trips HBM). */
+int pbn_step(pbn_batch *b, uint32_t n_updates);
+/* Philox mode, one launch applying n_updates in registers; bit-identical to pbn_step. */
+int pbn_rollout(pbn_batch *b, uint32_t n_updates);
+/* Replay mode: node_idx [T][B] (randint result) and k53 [T][B] (random() * 2^53), host arrays. */
+int pbn_step_replay(pbn_batch *b, const uint32_t *node_idx, const uint64_t *k53, uint32_t n_updates);
+/* MT mode: seeds [B] (host). random.seed(seeds[e]) (and np.random.seed for PROB_TABLE).
+ * init_state 1 also runs Graph.genRandState / PBN.reset(None) from that stream. */
+int pbn_mt_seed(pbn_batch *b, const uint64_t *seeds, int init_state);
+int pbn_mt_step(pbn_batch *b, uint32_t n_updates);
+
+/* ---- multi-flip until-attractor env step: PBNTargetMultiEnv.step (pbn_target_multi.py:119-154) ---- */
+int pbn_envcfg_create(const pbn_net *net, const pbn_envcfg_desc *desc, pbn_envcfg **out);
+void pbn_envcfg_destroy(pbn_envcfg *cfg);
+/* PBNTargetMultiEnv.reset (:227-259), Philox mode: envs with mask[e] != 0 (mask NULL = all)
+ * get a reset cube chosen uniformly, '*' bits drawn fair, n_steps = 0. */
+int pbn_env_reset(pbn_batch *b, const pbn_envcfg *cfg, const uint8_t *mask);
+int pbn_set_n_steps(pbn_batch *b, const int64_t *n_steps);  /* host [B] */
+int pbn_get_n_steps(pbn_batch *b, int64_t *n_steps);        /* host [B] */
+/* Host arrays: actions [B][A]; outputs obs [B][W], reward [B], flags [B], n_updates [B] (any may be NULL). */
+int pbn_env_step_multi(pbn_batch *b, const pbn_envcfg *cfg, const int32_t *actions, int A, int dedup, int offset,
+                       uint32_t update_cap, uint64_t *obs, int32_t *reward, uint8_t *flags, uint32_t *n_updates);
+/* Device arrays on the batch's device (e.g. torch tensors); asynchronous. */
+int pbn_env_step_multi_device(pbn_batch *b, const pbn_envcfg *cfg, const int32_t *d_actions, int A, int dedup,
+                              int offset, uint32_t update_cap, uint64_t *d_obs, int32_t *d_reward, uint8_t *d_flags,
+                              uint32_t *d_n_updates);
+/* Replay mode (parity): draw_offsets [B+1] (int64), draws_i / draws_k the reference's draws, host arrays. */
+int pbn_env_step_multi_replay(pbn_batch *b, const pbn_envcfg *cfg, const int32_t *actions, int A, int dedup,
+                              int offset, const int64_t *draw_offsets, const uint32_t *draws_i,
+                              const uint64_t *draws_k, uint64_t *obs, int32_t *reward, uint8_t *flags,
+                              uint32_t *n_updates);
+
+/* ---- measurement: HIP events on the batch stream around every kernel launch ---- */
+int pbn_timing_enable(pbn_batch *b, int enable);
+int pbn_timing_read(pbn_batch *b, double *kernel_ms, uint64_t *launches); /* syncs, then resets */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBN_ABI_H */

@@ -437,3 +437,33 @@ EXPORT int orc_env_step_multi(const orc_net *n, const orc_envcfg *c, uint64_t *s
     }
     return 0;
 }
+
+/* PBNTargetMultiEnv.reset (pbn_target_multi.py:237-249) in Philox mode: pick one of the
+ * reset cubes (all_attractors[0]) uniformly, keep its cared bits, draw the '*' bits fair. */
+EXPORT void orc_env_reset_philox(const orc_net *n, uint64_t *state, int64_t *n_steps, int64_t B,
+                                 const uint64_t *care, const uint64_t *value, int n_cubes, const uint8_t *mask,
+                                 uint64_t seed, uint64_t env_base, uint32_t reset_count) {
+    const int W = n->n_words;
+    for (int64_t e = 0; e < B; e++) {
+        if (mask && !mask[e]) continue;
+        uint64_t g = env_base + (uint64_t)e;
+        uint64_t *s = state + e * W;
+        for (int m = 0; 2 * m < W; m++) {
+            uint32_t w[4];
+            philox_draw(seed, (uint32_t)m + 1u, reset_count, g, STREAM_RESET, w);
+            s[2 * m] = ((uint64_t)w[1] << 32) | w[0];
+            if (2 * m + 1 < W) s[2 * m + 1] = ((uint64_t)w[3] << 32) | w[2];
+        }
+        uint32_t w[4];
+        philox_draw(seed, 0u, reset_count, g, STREAM_RESET, w);
+        uint32_t c = (uint32_t)(((uint64_t)w[0] * (uint32_t)n_cubes) >> 32);
+        for (int k = 0; k < W; k++) {
+            uint64_t cm = care[(int64_t)c * W + k];
+            s[k] = (value[(int64_t)c * W + k] & cm) | (s[k] & ~cm);
+        }
+        int r = n->n_nodes & 63;
+        if (r) s[W - 1] &= (((uint64_t)1 << r) - 1);
+        if (n->kind == 2) s[0] &= ~(uint64_t)1;
+        n_steps[e] = 0;
+    }
+}

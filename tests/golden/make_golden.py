@@ -336,7 +336,7 @@ def main():
         gen_r1_mt(base, "bittner199", T=3000)
     multi = refload.load_multi_env()
     if not only or "r6" in only:
-        gen_r6(base, multi, "bittner28", n_fixed=16, horizon=7, seeds=(1, 2, 3), n_steps=12, list_every=5)
+        gen_r6(base, multi, "bittner28", n_fixed=16, horizon=7, seeds=(1, 2, 3), n_steps=40, list_every=5)
         gen_r6(base, multi, "bittner199", n_fixed=165, horizon=100, seeds=(4, 5), n_steps=10)
     gen_cabean_kat(multi)
 
