@@ -89,6 +89,7 @@ def main():
     from gym_pbn_amd import _lib
     from gym_pbn_amd.batch import PBNBatch
     from gym_pbn_amd.network import load_network
+    from gym_pbn_amd.shard import max_over_ranks, shard_for
 
     dist = None
     if world > 1:
@@ -102,7 +103,8 @@ def main():
 
     net = load_network(args.network)
     B = args.batch
-    batch = PBNBatch(net, B, device=device, env_id_base=rank * B, seed=args.seed)
+    shard = shard_for(rank, world, B)  # contiguous global env ids; Philox keyed by global id
+    batch = PBNBatch(net, B, device=device, env_id_base=shard.env_base, seed=args.seed)
     batch.randomize()
     batch.sync()
 
@@ -121,35 +123,30 @@ def main():
     barrier()
     torch.cuda.synchronize()
     if not args.no_events:
-        batch.timing(True)
+        batch.timing(2)  # HIP events on the batch stream bracketing the timed launches
     t0 = time.perf_counter()
     batch.step(args.steps)
+    if not args.no_events:
+        batch.timing(0)  # closes the event region right behind the last launch
     batch.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     kernel_ms, launches = batch.timing_read() if not args.no_events else (float("nan"), 0)
-    batch.timing(False)
-    elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device=f"cuda:{device}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        k = torch.tensor([kernel_ms], device=f"cuda:{device}", dtype=torch.float64)
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kernel_ms = float(k.item())
+    elapsed = max_over_ranks(t1 - t0, dist, device=f"cuda:{device}")
+    kernel_ms = max_over_ranks(kernel_ms, dist, device=f"cuda:{device}")
 
     # supplementary: rollout mode (several updates per launch, state in registers)
     rollout = None
     if args.rollout > 1:
         batch.rollout(args.rollout)
         batch.sync()
-        batch.timing(True)
+        batch.timing(2)
         reps = 5
         for _ in range(reps):
             batch.rollout(args.rollout)
+        batch.timing(0)
         rms, rl = batch.timing_read()
-        batch.timing(False)
         rollout = {"updates_per_launch": args.rollout,
                    "node_updates_per_s_per_gpu": B * args.rollout * reps / (rms / 1e3),
                    "kernel_ms": rms / max(rl, 1)}
@@ -200,7 +197,8 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": "pbn::k_step<4,1,STORE_DIRTY,0>",
+                "kernel": "pbn::k_step<4,1,1,0> (W=4, predictor mix, dirty store, Philox)",
+                "timing": "HIP events on the batch stream bracketing the timed launches (launch gaps included)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
                 "traffic_source": pmc_src,

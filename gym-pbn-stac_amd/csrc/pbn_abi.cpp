@@ -133,11 +133,15 @@ struct pbn_batch {
     const void* d_image = nullptr;
     int n_cu = 0, bpc_step = 1, bpc_env = 1;
     int store_mode = STORE_DIRTY;
+    int envs_per_thread = 2;  // K: envs each thread walks per launch (pipelined)
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
-    // timing
-    bool timing = false;
+    // timing: mode 1 = an event pair around every launch; mode 2 = one region
+    // (start before the first launch after enabling, stop after the latest launch)
+    int timing = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
+    uint64_t region_launches = 0;
+    bool region_closed = false;
     int mt_ready = 0;
 
     int grid_for(uint64_t items, int bpc) const {
@@ -150,6 +154,18 @@ struct pbn_batch {
     int ev_begin(hipEvent_t* stop) {
         *stop = nullptr;
         if (!timing) return 0;
+        if (timing == 2) {
+            if (ev_pool.empty()) {
+                hipEvent_t a, b;
+                HIP_TRY(hipEventCreate(&a));
+                HIP_TRY(hipEventCreate(&b));
+                ev_pool.emplace_back(a, b);
+            }
+            if (region_launches == 0) HIP_TRY(hipEventRecord(ev_pool[0].first, stream));
+            region_launches++;
+            ev_used = 1;
+            return 0;  // the stop event is recorded once: pbn_timing_enable(0) or pbn_timing_read
+        }
         if (ev_used == ev_pool.size()) {
             hipEvent_t a, b;
             HIP_TRY(hipEventCreate(&a));
@@ -339,6 +355,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     b->env_base = env_id_base;
     b->seed = seed;
     if (const char* sm = getenv("PBNSIM_STORE_MODE")) b->store_mode = atoi(sm) ? STORE_DIRTY : STORE_FULL;
+    if (const char* r = getenv("PBNSIM_ENVS_PER_THREAD")) b->envs_per_thread = std::max(1, std::min(64, atoi(r)));
     hipDeviceProp_t prop;
     int rc = 0;
     auto bail = [&](int code) {
@@ -527,7 +544,9 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
     int store = (T == 1 && !replay) ? b->store_mode : STORE_FULL;
-    int e = launch_step(b->W, a, store, replay, b->grid_for(b->B, b->bpc_step), b->stream);
+    const uint64_t K = (uint64_t)b->envs_per_thread;
+    const uint64_t lanes = (b->B + K - 1) / K;
+    int e = launch_step(b->W, a, store, replay, b->grid_for(lanes, b->bpc_step), b->stream);
     if (e) return fail(PBN_E_HIP, "k_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);
 }
@@ -828,14 +847,26 @@ int pbn_env_step_multi_replay(pbn_batch* b, const pbn_envcfg* cfg_c, const int32
 // ------------------------------------------------------------------ timing
 int pbn_timing_enable(pbn_batch* b, int enable) {
     CHECK_NN(b, "batch");
-    b->timing = enable != 0;
+    if (enable < 0 || enable > 2) return fail(PBN_E_INVALID, "timing mode must be 0, 1 or 2");
+    if (b->timing == 2 && enable != 2) {
+        // close the open region right behind the last launch; pbn_timing_read reports it
+        if (b->region_launches) HIP_TRY(hipEventRecord(b->ev_pool[0].second, b->stream));
+        b->region_closed = true;
+        b->timing = enable;
+        return 0;
+    }
+    b->timing = enable;
     b->ev_used = 0;
+    b->region_launches = 0;
+    b->region_closed = false;
     return 0;
 }
 
 int pbn_timing_read(pbn_batch* b, double* kernel_ms, uint64_t* launches) {
     CHECK_NN(b, "batch");
     SET_DEV(b);
+    const bool region = b->timing == 2 || b->region_closed;
+    if (b->timing == 2 && b->region_launches) HIP_TRY(hipEventRecord(b->ev_pool[0].second, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     double tot = 0;
     for (size_t k = 0; k < b->ev_used; k++) {
@@ -844,8 +875,10 @@ int pbn_timing_read(pbn_batch* b, double* kernel_ms, uint64_t* launches) {
         tot += ms;
     }
     if (kernel_ms) *kernel_ms = tot;
-    if (launches) *launches = b->ev_used;
+    if (launches) *launches = region ? b->region_launches : b->ev_used;
     b->ev_used = 0;
+    b->region_launches = 0;
+    b->region_closed = false;
     return 0;
 }
 

@@ -21,17 +21,93 @@
 namespace pbn {
 
 // ------------------------------------------------------------------ step
+// Layout per workgroup in LDS: [network image][state planes]. The state planes
+// hold, for the env each lane is working on, its 2W dwords in planar order
+// (dword d of lane l at plane d, column l), so reading node i of the own env is
+// one conflict-free ds_read_b32 at plane (i >> 5) and an update is one
+// read-modify-write of one dword -- instead of ~20 VALU selects per bit when the
+// words sit in VGPRs. Columns are lane-private: no barrier is needed around them.
+//
+// Each thread walks envs e0, e0 + stride, ... with the next env's state load in
+// flight while the current env is computed (software pipeline), so HBM traffic
+// of one env overlaps the Philox/LDS work of the previous one.
+struct Plane {
+    uint32_t* base;  // &planes[0][tid]
+    __device__ __forceinline__ uint32_t get(uint32_t d) const { return base[d * BLOCK]; }
+    __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d * BLOCK] = v; }
+    __device__ __forceinline__ uint32_t bit(uint32_t i) const { return (get(i >> 5) >> (i & 31u)) & 1u; }
+};
+
+// Bittner Predstep (base.py:89-119) on the LDS plane; returns 1 if the bit changed.
+__device__ __forceinline__ uint32_t predictor_update_lds(const Plane& P, uint32_t i, uint64_t k53,
+                                                         const uint8_t* tbl, const NetLayout& L) {
+    const uint32_t info = reinterpret_cast<const uint32_t*>(tbl + L.off_node)[i];
+    const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
+    const uint64_t* thr = reinterpret_cast<const uint64_t*>(tbl + L.off_thr) + o0;
+    uint32_t j = 0;
+#pragma unroll 4
+    for (uint32_t q = 0; q + 1 < cnt; ++q) j += (k53 >= thr[q]) ? 1u : 0u;
+    const uint64_t rec = reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[o0 + j];
+    const uint32_t d = i >> 5, sh = i & 31u;
+    const uint32_t self = P.get(d);
+    const uint32_t p = (P.bit((uint32_t)rec & 0xFFFFu) << 3) | (P.bit((uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
+                       (P.bit((uint32_t)(rec >> 32) & 0xFFFFu) << 1) | ((self >> sh) & 1u);
+    const uint32_t y = (uint32_t)(rec >> (48 + p)) & 1u;
+    const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+    P.put(d, nv);
+    return nv != self;
+}
+
+// PBN node update (common/node.py:31-38) on the LDS plane.
+__device__ __forceinline__ uint32_t table_update_lds(const Plane& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
+                                                     const NetLayout& L) {
+    const uint64_t info = reinterpret_cast<const uint64_t*>(tbl + L.off_node)[i];
+    const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu, k = (uint32_t)(info >> 48) & 0xFFu;
+    const uint16_t* in = reinterpret_cast<const uint16_t*>(tbl + L.off_rec) + ioff;
+    uint32_t idx = 0;
+#pragma unroll 4
+    for (uint32_t q = 0; q < k; ++q) idx = (idx << 1) | P.bit(in[q]);
+    const uint64_t t = reinterpret_cast<const uint64_t*>(tbl + L.off_thr)[toff + idx];
+    const uint32_t y = k53 < t ? 1u : 0u;
+    const uint32_t d = i >> 5, sh = i & 31u;
+    const uint32_t self = P.get(d);
+    const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+    P.put(d, nv);
+    return nv != self;
+}
+
+template <int W>
+__device__ __forceinline__ void to_plane(const Plane& P, const uint64_t (&s)[W]) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        P.put(2 * k, (uint32_t)s[k]);
+        P.put(2 * k + 1, (uint32_t)(s[k] >> 32));
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void from_plane(const Plane& P, uint64_t (&s)[W]) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) s[k] = (uint64_t)P.get(2 * k) | ((uint64_t)P.get(2 * k + 1) << 32);
+}
+
 template <int W, int KIND, int STORE, int REPLAY>
 __global__ __launch_bounds__(BLOCK) void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t cur[W];
+    if (e < a.B) load_state<W>(a.state + e * W, cur);
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
+    const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     const uint32_t N = (uint32_t)a.L.n_nodes;
-    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < a.B; e += stride) {
-        uint64_t s[W];
-        load_state<W>(a.state + e * W, s);
-        uint32_t dirty = 0;
+    while (e < a.B) {
+        const uint64_t en = e + stride;
+        uint64_t nxt[W];
+        if (en < a.B) load_state<W>(a.state + en * W, nxt);  // prefetch the next env
+        to_plane<W>(P, cur);
+        uint32_t changed = 0;
         const uint64_t g = a.env_base + e;
         for (uint32_t t = 0; t < a.T; ++t) {
             uint32_t i;
@@ -46,14 +122,24 @@ __global__ __launch_bounds__(BLOCK) void k_step(StepArgs a) {
                 i = philox_node<KIND>(w[0], N);
                 k53 = k53_of(w[1], w[2]);
             }
-            const uint32_t old = getbit<W>(s, i);
-            const uint32_t y = node_update<W, KIND>(s, i, k53, lds, a.L);
-            dirty |= (old != y ? 1u : 0u) << (i >> 6);
+            if constexpr (KIND == KIND_PREDICTOR_MIX)
+                changed |= predictor_update_lds(P, i, k53, lds, a.L);
+            else
+                changed |= table_update_lds(P, i, k53, lds, a.L);
         }
-        if constexpr (STORE == STORE_DIRTY)
-            store_dirty<W>(a.state + e * W, s, dirty);
-        else
-            store_state<W>(a.state + e * W, s);
+        uint64_t out[W];
+        from_plane<W>(P, out);
+        if constexpr (STORE == STORE_DIRTY) {
+            uint32_t dirty = 0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) dirty |= (out[k] != cur[k] ? 1u : 0u) << k;
+            if (changed) store_dirty<W>(a.state + e * W, out, dirty);
+        } else {
+            store_state<W>(a.state + e * W, out);
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) cur[k] = nxt[k];
+        e = en;
     }
 }
 
@@ -302,11 +388,13 @@ static int launch(void* fn, int grid, uint32_t lds, void* stream, void* args, si
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
 }
 
+uint32_t step_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK; }
+
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream) {
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay)
                                               : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay);
     StepArgs c = a;
-    return launch(fn, grid, a.L.bytes, stream, &c, sizeof c);
+    return launch(fn, grid, step_lds_bytes(W, a.L.bytes), stream, &c, sizeof c);
 }
 
 int launch_init(int W, const InitArgs& a, int grid, void* stream) {
@@ -337,7 +425,7 @@ static int occupancy(void* fn, uint32_t lds, int* blocks_per_cu) {
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
     void* fn = kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, STORE_FULL, 0)
                                           : step_fn_w<KIND_PROB_TABLE>(W, STORE_FULL, 0);
-    return occupancy(fn, lds_bytes, blocks_per_cu);
+    return occupancy(fn, step_lds_bytes(W, lds_bytes), blocks_per_cu);
 }
 
 int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {

@@ -10,7 +10,7 @@ enum { STORE_FULL = 0, STORE_DIRTY = 1 };
 
 constexpr int BLOCK = 256;          // 4 wave64 per workgroup
 constexpr int MAX_WORDS = 8;        // N <= 512
-constexpr uint32_t MAX_IMAGE = 64 * 1024;  // LDS bytes for the network image
+constexpr uint32_t MAX_IMAGE = 48 * 1024;  // LDS bytes for the network image (+ 16 KiB state planes)
 
 // Byte offsets of the tables inside the LDS image (16-byte aligned image).
 struct NetLayout {
@@ -80,6 +80,7 @@ struct EnvArgs {
 
 // Launchers (pbn_kernels.hip). Return hipError_t as int.
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream);
+uint32_t step_lds_bytes(int W, uint32_t image_bytes);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);

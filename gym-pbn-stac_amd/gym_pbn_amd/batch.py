@@ -296,8 +296,9 @@ class PBNBatch:
                                                 C.c_void_p(d_n_updates)))
 
     # -- timing -----------------------------------------------------------
-    def timing(self, enable: bool):
-        L.check(L.lib.pbn_timing_enable(self._h, int(bool(enable))))
+    def timing(self, mode):
+        """0 off; 1 an event pair around every launch; 2 one event region over all launches."""
+        L.check(L.lib.pbn_timing_enable(self._h, int(mode)))
 
     def timing_read(self):
         ms = C.c_double(0)

@@ -170,7 +170,8 @@ int pbn_env_step_multi_replay(pbn_batch *b, const pbn_envcfg *cfg, const int32_t
                               const uint64_t *draws_k, uint64_t *obs, int32_t *reward, uint8_t *flags,
                               uint32_t *n_updates);
 
-/* ---- measurement: HIP events on the batch stream around every kernel launch ---- */
+/* ---- measurement: HIP events on the batch stream. mode 1: a pair around every kernel launch;
+ *      mode 2: one region from before the first launch to after the last (launch gaps included) ---- */
 int pbn_timing_enable(pbn_batch *b, int enable);
 int pbn_timing_read(pbn_batch *b, double *kernel_ms, uint64_t *launches); /* syncs, then resets */
 

@@ -1,0 +1,79 @@
+"""The N>1 path on CPU: world_size-2 gloo processes (no GPU).
+
+Each rank steps its contiguous shard of global env ids (here with the oracle,
+the same Philox stream the kernels use), then the trajectory chunks are
+all-gathered; the result must equal one process stepping the whole batch.
+This is the partitioning bench.py uses across GPUs (weak scaling, no
+collective in the stepping path).
+"""
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_local, T, out_dir):
+    sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    import oracle as O
+    from gym_pbn_amd.network import load_network
+    from gym_pbn_amd.shard import gather_chunks, max_over_ranks, shard_for
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = shard_for(rank, world, n_local)
+    o = O.Oracle(load_network("bittner28"))
+    st = o.init_philox(n_local, seed=99, env_base=sh.env_base)
+    chunk = np.empty((n_local, T, o.W), dtype=np.uint64)
+    for t in range(T):
+        st = o.step_philox(st, 99, sh.env_base, t, 1)
+        chunk[:, t] = st
+    full = gather_chunks(chunk, dist)
+    slowest = max_over_ranks(float(rank + 1), dist)
+    if rank == 0:
+        np.save(Path(out_dir) / "gathered.npy", full)
+        np.save(Path(out_dir) / "slowest.npy", np.array([slowest]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_match_single_process(tmp_path, oracle_mod):
+    from gym_pbn_amd.network import load_network
+
+    n_local, T, world = 300, 12, 2
+    mp.spawn(_worker, args=(world, _free_port(), n_local, T, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(tmp_path / "gathered.npy")
+    o = oracle_mod.Oracle(load_network("bittner28"))
+    st = o.init_philox(world * n_local, seed=99, env_base=0)
+    ref = np.empty_like(got)
+    for t in range(T):
+        st = o.step_philox(st, 99, 0, t, 1)
+        ref[:, t] = st
+    assert np.array_equal(got, ref)
+    assert float(np.load(tmp_path / "slowest.npy")[0]) == 2.0
+
+
+def test_shard_ranges():
+    sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
+    from gym_pbn_amd.shard import shard_for
+
+    shards = [shard_for(r, 8, 1 << 20) for r in range(8)]
+    assert [s.env_base for s in shards] == [r << 20 for r in range(8)]
+    assert shards[0].n_global == 8 << 20
