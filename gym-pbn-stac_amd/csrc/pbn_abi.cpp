@@ -135,6 +135,7 @@ struct pbn_batch {
     int store_mode = STORE_DIRTY;
     int envs_per_thread = 2;  // K: envs each thread walks per launch (pipelined)
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
+    DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     // timing: mode 1 = an event pair around every launch; mode 2 = one region
     // (start before the first launch after enabling, stop after the latest launch)
     int timing = 0;
@@ -394,7 +395,7 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_nsteps) (void)hipFree(b->d_nsteps);
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
-                      &b->s_off, &b->s_mask})
+                      &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds})
         d->release();
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -592,18 +593,63 @@ int pbn_step_replay(pbn_batch* b, const uint32_t* node_idx, const uint64_t* k53,
     return 0;
 }
 
+static MTArgs mt_args(pbn_batch* b) {
+    MTArgs a{};
+    a.state = b->d_state;
+    a.img = b->d_image;
+    a.L = b->net->L;
+    a.B = b->B;
+    a.n_nodes = b->N;
+    a.mt_py = (uint32_t*)b->mt_py.p;
+    a.mt_np = (uint32_t*)b->mt_np.p;
+    a.pos_py = (uint32_t*)b->mt_pos_py.p;
+    a.pos_np = (uint32_t*)b->mt_pos_np.p;
+    return a;
+}
+
 int pbn_mt_seed(pbn_batch* b, const uint64_t* seeds, int init_state) {
-    (void)seeds;
-    (void)init_state;
     CHECK_NN(b, "batch");
-    return fail(PBN_E_UNSUPPORTED, "MT mode is not built into this library version");
+    CHECK_NN(seeds, "seeds");
+    const bool table = b->net->kind == PBN_KIND_PROB_TABLE;
+    if (table)  // np.random.seed(s) accepts 0 <= s < 2^32 only
+        for (uint64_t e = 0; e < b->B; e++)
+            if (seeds[e] >> 32) return fail(PBN_E_RANGE, "Seed must be between 0 and 2**32 - 1 (env %llu)",
+                                            (unsigned long long)e);
+    SET_DEV(b);
+    const size_t row = 4 * (size_t)MT_ROW * b->B;
+    if (int rc = b->mt_py.ensure(row)) return rc;
+    if (int rc = b->mt_pos_py.ensure(4 * b->B)) return rc;
+    if (table) {
+        if (int rc = b->mt_np.ensure(row)) return rc;
+        if (int rc = b->mt_pos_np.ensure(4 * b->B)) return rc;
+    }
+    if (int rc = b->mt_seeds.ensure(8 * b->B)) return rc;
+    HIP_TRY(hipMemcpyAsync(b->mt_seeds.p, seeds, 8 * b->B, hipMemcpyHostToDevice, b->stream));
+    MTArgs a = mt_args(b);
+    a.seeds = (const uint64_t*)b->mt_seeds.p;
+    a.init_state = init_state ? 1 : 0;
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int e = launch_mt_seed(b->W, a, b->grid_all(b->B), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_mt_seed launch: %s", hipGetErrorString((hipError_t)e));
+    if (int rc = b->ev_end(stop)) return rc;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    b->mt_ready = 1;
+    return 0;
 }
 
 int pbn_mt_step(pbn_batch* b, uint32_t n_updates) {
-    (void)n_updates;
     CHECK_NN(b, "batch");
     if (!b->mt_ready) return fail(PBN_E_STATE, "pbn_mt_seed has not been called");
-    return fail(PBN_E_UNSUPPORTED, "MT mode is not built into this library version");
+    if (!n_updates) return 0;
+    SET_DEV(b);
+    MTArgs a = mt_args(b);
+    a.T = n_updates;
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int e = launch_mt_step(b->W, a, b->grid_for(b->B, b->bpc_step), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_mt_step launch: %s", hipGetErrorString((hipError_t)e));
+    return b->ev_end(stop);
 }
 
 // ------------------------------------------------------------------ R6 env

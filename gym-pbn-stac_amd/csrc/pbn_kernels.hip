@@ -31,66 +31,6 @@ namespace pbn {
 // Each thread walks envs e0, e0 + stride, ... with the next env's state load in
 // flight while the current env is computed (software pipeline), so HBM traffic
 // of one env overlaps the Philox/LDS work of the previous one.
-struct Plane {
-    uint32_t* base;  // &planes[0][tid]
-    __device__ __forceinline__ uint32_t get(uint32_t d) const { return base[d * BLOCK]; }
-    __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d * BLOCK] = v; }
-    __device__ __forceinline__ uint32_t bit(uint32_t i) const { return (get(i >> 5) >> (i & 31u)) & 1u; }
-};
-
-// Bittner Predstep (base.py:89-119) on the LDS plane; returns 1 if the bit changed.
-__device__ __forceinline__ uint32_t predictor_update_lds(const Plane& P, uint32_t i, uint64_t k53,
-                                                         const uint8_t* tbl, const NetLayout& L) {
-    const uint32_t info = reinterpret_cast<const uint32_t*>(tbl + L.off_node)[i];
-    const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
-    const uint64_t* thr = reinterpret_cast<const uint64_t*>(tbl + L.off_thr) + o0;
-    uint32_t j = 0;
-#pragma unroll 4
-    for (uint32_t q = 0; q + 1 < cnt; ++q) j += (k53 >= thr[q]) ? 1u : 0u;
-    const uint64_t rec = reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[o0 + j];
-    const uint32_t d = i >> 5, sh = i & 31u;
-    const uint32_t self = P.get(d);
-    const uint32_t p = (P.bit((uint32_t)rec & 0xFFFFu) << 3) | (P.bit((uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
-                       (P.bit((uint32_t)(rec >> 32) & 0xFFFFu) << 1) | ((self >> sh) & 1u);
-    const uint32_t y = (uint32_t)(rec >> (48 + p)) & 1u;
-    const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-    P.put(d, nv);
-    return nv != self;
-}
-
-// PBN node update (common/node.py:31-38) on the LDS plane.
-__device__ __forceinline__ uint32_t table_update_lds(const Plane& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
-                                                     const NetLayout& L) {
-    const uint64_t info = reinterpret_cast<const uint64_t*>(tbl + L.off_node)[i];
-    const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu, k = (uint32_t)(info >> 48) & 0xFFu;
-    const uint16_t* in = reinterpret_cast<const uint16_t*>(tbl + L.off_rec) + ioff;
-    uint32_t idx = 0;
-#pragma unroll 4
-    for (uint32_t q = 0; q < k; ++q) idx = (idx << 1) | P.bit(in[q]);
-    const uint64_t t = reinterpret_cast<const uint64_t*>(tbl + L.off_thr)[toff + idx];
-    const uint32_t y = k53 < t ? 1u : 0u;
-    const uint32_t d = i >> 5, sh = i & 31u;
-    const uint32_t self = P.get(d);
-    const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-    P.put(d, nv);
-    return nv != self;
-}
-
-template <int W>
-__device__ __forceinline__ void to_plane(const Plane& P, const uint64_t (&s)[W]) {
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-        P.put(2 * k, (uint32_t)s[k]);
-        P.put(2 * k + 1, (uint32_t)(s[k] >> 32));
-    }
-}
-
-template <int W>
-__device__ __forceinline__ void from_plane(const Plane& P, uint64_t (&s)[W]) {
-#pragma unroll
-    for (int k = 0; k < W; ++k) s[k] = (uint64_t)P.get(2 * k) | ((uint64_t)P.get(2 * k + 1) << 32);
-}
-
 template <int W, int KIND, int STORE, int REPLAY>
 __global__ __launch_bounds__(BLOCK) void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];

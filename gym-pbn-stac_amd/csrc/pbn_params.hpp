@@ -78,7 +78,24 @@ struct EnvArgs {
     const uint64_t* draws_k;
 };
 
-// Launchers (pbn_kernels.hip). Return hipError_t as int.
+constexpr uint32_t MT_ROW = 624;  // u32 words of one MT19937 state row
+
+struct MTArgs {
+    uint64_t* state;        // [B][W]
+    const void* img;        // network image
+    NetLayout L;
+    uint64_t B;
+    uint32_t T;             // transitions per launch (k_mt_step)
+    int32_t n_nodes;
+    int32_t init_state;     // k_mt_seed: also run genRandState / PBN.reset(None)
+    const uint64_t* seeds;  // [B] (k_mt_seed)
+    uint32_t* mt_py;        // [B][MT_ROW] CPython `random` state
+    uint32_t* mt_np;        // [B][MT_ROW] numpy legacy RandomState (probability-table networks)
+    uint32_t* pos_py;       // [B] next word index (624 = twist before next use)
+    uint32_t* pos_np;
+};
+
+// Launchers (pbn_kernels.hip, pbn_mt.hip). Return hipError_t as int.
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream);
 uint32_t step_lds_bytes(int W, uint32_t image_bytes);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
@@ -86,5 +103,7 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
 int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
+int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
+int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 
 }  // namespace pbn

@@ -147,7 +147,7 @@ int pbn_step_replay(pbn_batch *b, const uint32_t *node_idx, const uint64_t *k53,
 /* MT mode: seeds [B] (host). random.seed(seeds[e]) (and np.random.seed for PROB_TABLE).
  * init_state 1 also runs Graph.genRandState / PBN.reset(None) from that stream. */
 int pbn_mt_seed(pbn_batch *b, const uint64_t *seeds, int init_state);
-int pbn_mt_step(pbn_batch *b, uint32_t n_updates);
+int pbn_mt_step(pbn_batch *b, uint32_t n_updates); /* asynchronous; seeds >= 2^32 rejected for PROB_TABLE */
 
 /* ---- multi-flip until-attractor env step: PBNTargetMultiEnv.step (pbn_target_multi.py:119-154) ---- */
 int pbn_envcfg_create(const pbn_net *net, const pbn_envcfg_desc *desc, pbn_envcfg **out);

@@ -214,3 +214,48 @@ def test_vec_env_and_single_env_adapters(G):
     assert sum(a != b for a, b in zip(s0, s1)) <= 1
     with pytest.raises(ValueError):
         g.flipNode(28)
+
+
+# ----------------------------------------------------------------- MT mode: reference streams on device
+@pytest.mark.parametrize("name", ["bittner28", "bittner199"])
+def test_mt_mode_reproduces_reference_from_seed(G, name):
+    """random.seed(s); genRandState(); T x Graph.step() -- reproduced on the GPU from s alone."""
+    z = golden(f"r1_mt_{name}.npz")
+    b = G.PBNBatch(name, len(z["seeds"]))
+    b.mt_seed(z["seeds"], init_state=True)
+    assert np.array_equal(b.get_state(), z["init"])
+    cp = z["checkpoints"]
+    for k in range(cp.shape[1]):
+        b.mt_step(1000)
+        assert np.array_equal(b.get_state(), cp[:, k]), k
+    assert np.array_equal(b.get_state(), z["final"])
+
+
+@pytest.mark.parametrize("name", ["tt200", "tt8"])
+def test_mt_mode_truth_table_reproduces_reference(G, name):
+    """random.seed(s); np.random.seed(s); PBN.reset(); T x PBN.step() on the GPU."""
+    z = golden(f"r4_{name}.npz")
+    b = G.PBNBatch(name, len(z["seeds"]))
+    b.mt_seed(z["seeds"], init_state=True)
+    assert np.array_equal(b.get_state(), z["init"])
+    T = z["states"].shape[1]
+    b.mt_step(7)
+    assert np.array_equal(b.get_state(), z["states"][:, 6])
+    b.mt_step(T - 7)
+    assert np.array_equal(b.get_state(), z["states"][:, -1])
+
+
+def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
+    """65,536 envs seeded 0..65535 (crossing many MT twists); sampled envs vs the oracle's CPython MT."""
+    net = load_network("bittner199")
+    B, T = 65536, 700
+    seeds = np.arange(B, dtype=np.uint64) * np.uint64(2654435761) + np.uint64(3)
+    b = G.PBNBatch(net, B)
+    b.mt_seed(seeds, init_state=True)
+    b.mt_step(T)
+    got = b.get_state()
+    o = oracle_mod.Oracle(net)
+    idx = np.random.default_rng(1).choice(B, 64, replace=False)
+    assert np.array_equal(got[idx], o.run_mt(seeds[idx], T))
+    with pytest.raises(ValueError):
+        G.PBNBatch("tt8", 2).mt_seed(np.array([1, 2**33], dtype=np.uint64))
