@@ -197,7 +197,7 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": "pbn::k_step<4,1,1,0> (W=4, predictor mix, dirty store, Philox)",
+                "kernel": "pbn::k_step<4,1,1,0,1024> (W=4, predictor mix, dirty store, Philox, 1024-thread groups)",
                 "timing": "HIP events on the batch stream bracketing the timed launches (launch gaps included)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,

@@ -131,7 +131,8 @@ struct pbn_batch {
     int64_t* d_nsteps = nullptr;
     int32_t* d_error = nullptr;
     const void* d_image = nullptr;
-    int n_cu = 0, bpc_step = 1, bpc_env = 1;
+    int n_cu = 0, bpc_step = 1, bpc_env = 1, bpc_base = 1;
+    int step_block = 1024;  // threads per workgroup of the Philox step kernel (256 or 1024)
     int store_mode = STORE_DIRTY;
     int envs_per_thread = 2;  // K: envs each thread walks per launch (pipelined)
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
@@ -145,8 +146,8 @@ struct pbn_batch {
     bool region_closed = false;
     int mt_ready = 0;
 
-    int grid_for(uint64_t items, int bpc) const {
-        uint64_t need = (items + BLOCK - 1) / BLOCK;
+    int grid_for(uint64_t items, int bpc, int block = BLOCK) const {
+        uint64_t need = (items + block - 1) / block;
         uint64_t cap = (uint64_t)n_cu * (uint64_t)bpc;
         uint64_t g = std::min<uint64_t>(need, cap);
         return (int)std::max<uint64_t>(g, 1);
@@ -365,6 +366,9 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     };
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PBN_E_HIP, "hipGetDeviceProperties"));
     b->n_cu = prop.multiProcessorCount;
+    if (const char* sbv = getenv("PBNSIM_STEP_BLOCK")) b->step_block = atoi(sbv) == 256 ? 256 : 1024;
+    else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
+        b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(PBN_E_HIP, "hipStreamCreate"));
     size_t sb = 8 * (size_t)b->W * n_envs;
@@ -376,7 +380,9 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
         return bail(fail(PBN_E_HIP, "hipMemset"));
     b->d_image = net->image_on(device);
     if (!b->d_image) return bail(fail(PBN_E_NOMEM, "network image upload failed"));
-    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, &b->bpc_step)))
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, BLOCK, &b->bpc_base)))
+        return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, b->step_block, &b->bpc_step)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
     if (hipStreamSynchronize(b->stream) != hipSuccess) return bail(fail(PBN_E_HIP, "stream sync"));
     *out = b;
@@ -547,7 +553,9 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
     int store = (T == 1 && !replay) ? b->store_mode : STORE_FULL;
     const uint64_t K = (uint64_t)b->envs_per_thread;
     const uint64_t lanes = (b->B + K - 1) / K;
-    int e = launch_step(b->W, a, store, replay, b->grid_for(lanes, b->bpc_step), b->stream);
+    const int sb = replay ? BLOCK : b->step_block;
+    const int grid = replay ? b->grid_for(lanes, b->bpc_base) : b->grid_for(lanes, b->bpc_step, sb);
+    int e = launch_step(b->W, a, store, replay, sb, grid, b->stream);
     if (e) return fail(PBN_E_HIP, "k_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);
 }
@@ -647,7 +655,7 @@ int pbn_mt_step(pbn_batch* b, uint32_t n_updates) {
     a.T = n_updates;
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
-    int e = launch_mt_step(b->W, a, b->grid_for(b->B, b->bpc_step), b->stream);
+    int e = launch_mt_step(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
     if (e) return fail(PBN_E_HIP, "k_mt_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);
 }

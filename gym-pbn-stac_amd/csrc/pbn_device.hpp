@@ -185,15 +185,19 @@ __device__ __forceinline__ uint32_t philox_node(uint32_t w0, uint32_t N) {
 }
 
 // ---------------------------------------------------------------- LDS state planes
-struct Plane {
+// SB = lanes per workgroup = the plane's row stride (dword d of lane l at d*SB + l).
+template <int SB>
+struct PlaneT {
     uint32_t* base;  // &planes[0][tid]
-    __device__ __forceinline__ uint32_t get(uint32_t d) const { return base[d * BLOCK]; }
-    __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d * BLOCK] = v; }
+    __device__ __forceinline__ uint32_t get(uint32_t d) const { return base[d * SB]; }
+    __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d * SB] = v; }
     __device__ __forceinline__ uint32_t bit(uint32_t i) const { return (get(i >> 5) >> (i & 31u)) & 1u; }
 };
+using Plane = PlaneT<BLOCK>;
 
 // Bittner Predstep (base.py:89-119) on the LDS plane; returns 1 if the bit changed.
-__device__ __forceinline__ uint32_t predictor_update_lds(const Plane& P, uint32_t i, uint64_t k53,
+template <class P_t>
+__device__ __forceinline__ uint32_t predictor_update_lds(const P_t& P, uint32_t i, uint64_t k53,
                                                          const uint8_t* tbl, const NetLayout& L) {
     const uint32_t info = reinterpret_cast<const uint32_t*>(tbl + L.off_node)[i];
     const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
@@ -213,7 +217,8 @@ __device__ __forceinline__ uint32_t predictor_update_lds(const Plane& P, uint32_
 }
 
 // PBN node update (common/node.py:31-38) on the LDS plane.
-__device__ __forceinline__ uint32_t table_update_lds(const Plane& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
+template <class P_t>
+__device__ __forceinline__ uint32_t table_update_lds(const P_t& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
                                                      const NetLayout& L) {
     const uint64_t info = reinterpret_cast<const uint64_t*>(tbl + L.off_node)[i];
     const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu, k = (uint32_t)(info >> 48) & 0xFFu;
@@ -230,8 +235,8 @@ __device__ __forceinline__ uint32_t table_update_lds(const Plane& P, uint32_t i,
     return nv != self;
 }
 
-template <int W>
-__device__ __forceinline__ void to_plane(const Plane& P, const uint64_t (&s)[W]) {
+template <int W, class P_t>
+__device__ __forceinline__ void to_plane(const P_t& P, const uint64_t (&s)[W]) {
 #pragma unroll
     for (int k = 0; k < W; ++k) {
         P.put(2 * k, (uint32_t)s[k]);
@@ -239,8 +244,8 @@ __device__ __forceinline__ void to_plane(const Plane& P, const uint64_t (&s)[W])
     }
 }
 
-template <int W>
-__device__ __forceinline__ void from_plane(const Plane& P, uint64_t (&s)[W]) {
+template <int W, class P_t>
+__device__ __forceinline__ void from_plane(const P_t& P, uint64_t (&s)[W]) {
 #pragma unroll
     for (int k = 0; k < W; ++k) s[k] = (uint64_t)P.get(2 * k) | ((uint64_t)P.get(2 * k + 1) << 32);
 }

@@ -31,16 +31,20 @@ namespace pbn {
 // Each thread walks envs e0, e0 + stride, ... with the next env's state load in
 // flight while the current env is computed (software pipeline), so HBM traffic
 // of one env overlaps the Philox/LDS work of the previous one.
-template <int W, int KIND, int STORE, int REPLAY>
-__global__ __launch_bounds__(BLOCK) void k_step(StepArgs a) {
+//
+// SB (threads per workgroup) trades LDS staging traffic against scheduling
+// granularity: the image is staged once per workgroup, so 1024-thread groups
+// read it from L2 4x less often than 256-thread groups.
+template <int W, int KIND, int STORE, int REPLAY, int SB>
+__global__ __launch_bounds__(SB) void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
-    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * SB;
+    uint64_t e = (uint64_t)blockIdx.x * SB + threadIdx.x;
     uint64_t cur[W];
     if (e < a.B) load_state<W>(a.state + e * W, cur);
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
-    const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     const uint32_t N = (uint32_t)a.L.n_nodes;
     while (e < a.B) {
         const uint64_t en = e + stride;
@@ -255,22 +259,26 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 
 // ------------------------------------------------------------------ dispatch
 template <int W, int KIND>
-static void* step_fn(int store, int replay) {
-    if (replay) return (void*)k_step<W, KIND, STORE_FULL, 1>;
-    return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0> : (void*)k_step<W, KIND, STORE_FULL, 0>;
+static void* step_fn(int store, int replay, int sb) {
+    if (replay) return (void*)k_step<W, KIND, STORE_FULL, 1, BLOCK>;
+    if (sb == 1024)
+        return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0, 1024>
+                                    : (void*)k_step<W, KIND, STORE_FULL, 0, 1024>;
+    return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0, BLOCK>
+                                : (void*)k_step<W, KIND, STORE_FULL, 0, BLOCK>;
 }
 
 template <int KIND>
-static void* step_fn_w(int W, int store, int replay) {
+static void* step_fn_w(int W, int store, int replay, int sb) {
     switch (W) {
-        case 1: return step_fn<1, KIND>(store, replay);
-        case 2: return step_fn<2, KIND>(store, replay);
-        case 3: return step_fn<3, KIND>(store, replay);
-        case 4: return step_fn<4, KIND>(store, replay);
-        case 5: return step_fn<5, KIND>(store, replay);
-        case 6: return step_fn<6, KIND>(store, replay);
-        case 7: return step_fn<7, KIND>(store, replay);
-        case 8: return step_fn<8, KIND>(store, replay);
+        case 1: return step_fn<1, KIND>(store, replay, sb);
+        case 2: return step_fn<2, KIND>(store, replay, sb);
+        case 3: return step_fn<3, KIND>(store, replay, sb);
+        case 4: return step_fn<4, KIND>(store, replay, sb);
+        case 5: return step_fn<5, KIND>(store, replay, sb);
+        case 6: return step_fn<6, KIND>(store, replay, sb);
+        case 7: return step_fn<7, KIND>(store, replay, sb);
+        case 8: return step_fn<8, KIND>(store, replay, sb);
     }
     return nullptr;
 }
@@ -328,13 +336,28 @@ static int launch(void* fn, int grid, uint32_t lds, void* stream, void* args, si
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
 }
 
-uint32_t step_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK; }
+uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb) {
+    return image_bytes + 8u * (uint32_t)W * (uint32_t)sb;
+}
 
-int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream) {
-    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay)
-                                              : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay);
+static void* step_kernel(int W, int kind, int store_mode, int replay, int sb) {
+    if (replay) sb = BLOCK;
+    return kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay, sb)
+                                      : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay, sb);
+}
+
+int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream) {
+    if (replay) sb = BLOCK;
+    void* fn = step_kernel(W, a.L.kind, store_mode, replay, sb);
+    if (!fn) return (int)hipErrorInvalidValue;
+    const uint32_t lds = step_lds_bytes(W, a.L.bytes, sb);
+    if (lds > 64u * 1024u) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+    }
     StepArgs c = a;
-    return launch(fn, grid, step_lds_bytes(W, a.L.bytes), stream, &c, sizeof c);
+    void* kargs[] = {&c};
+    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3((unsigned)sb), kargs, lds, (hipStream_t)stream);
 }
 
 int launch_init(int W, const InitArgs& a, int grid, void* stream) {
@@ -354,23 +377,26 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
     return launch(fn, grid, a.L.bytes, stream, &c, sizeof c);
 }
 
-static int occupancy(void* fn, uint32_t lds, int* blocks_per_cu) {
+static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
     int nb = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, BLOCK, lds);
+    if (lds > 64u * 1024u) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+    }
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, block, lds);
     if (e != hipSuccess) return (int)e;
     *blocks_per_cu = nb < 1 ? 1 : nb;
     return 0;
 }
 
-int max_blocks_step(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
-    void* fn = kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, STORE_FULL, 0)
-                                          : step_fn_w<KIND_PROB_TABLE>(W, STORE_FULL, 0);
-    return occupancy(fn, step_lds_bytes(W, lds_bytes), blocks_per_cu);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu) {
+    void* fn = step_kernel(W, kind, STORE_FULL, 0, sb);
+    return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb), blocks_per_cu);
 }
 
 int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
     void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0) : env_fn_w<KIND_PROB_TABLE>(W, 0);
-    return occupancy(fn, lds_bytes, blocks_per_cu);
+    return occupancy(fn, BLOCK, lds_bytes, blocks_per_cu);
 }
 
 }  // namespace pbn

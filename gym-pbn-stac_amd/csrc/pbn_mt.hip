@@ -222,7 +222,7 @@ int launch_mt_step(int W, const MTArgs& a, int grid, void* stream) {
     if (!fn) return (int)hipErrorInvalidValue;
     MTArgs c = a;
     void* kargs[] = {&c};
-    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, step_lds_bytes(W, a.L.bytes),
+    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, step_lds_bytes(W, a.L.bytes, BLOCK),
                                 (hipStream_t)stream);
 }
 

@@ -96,12 +96,12 @@ struct MTArgs {
 };
 
 // Launchers (pbn_kernels.hip, pbn_mt.hip). Return hipError_t as int.
-int launch_step(int W, const StepArgs& a, int store_mode, int replay, int grid, void* stream);
-uint32_t step_lds_bytes(int W, uint32_t image_bytes);
+int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream);
+uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
-int max_blocks_step(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
 int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
