@@ -91,7 +91,7 @@ struct pbn_envcfg {
     int W = 0, H = 0, H_reset = 0;
     std::vector<uint8_t> image;  // net image + cubes [H][2][W] + target [2][W]
     NetLayout L{};
-    uint32_t off_cubes = 0, off_target = 0;
+    uint32_t off_cubes = 0, off_target = 0, off_nodemask = 0;
     std::vector<uint64_t> reset_care, reset_value;
     int32_t horizon = 100, reward_success = 1000, action_cost = 1;
     std::mutex mu;
@@ -137,6 +137,7 @@ struct pbn_batch {
     int envs_per_thread = 2;  // K: envs each thread walks per launch (pipelined)
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
+    DevBuf s_counter;                                     // env-step work-queue head
     // timing: mode 1 = an event pair around every launch; mode 2 = one region
     // (start before the first launch after enabling, stop after the latest launch)
     int timing = 0;
@@ -401,7 +402,8 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_nsteps) (void)hipFree(b->d_nsteps);
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
-                      &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds})
+                      &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
+                      &b->s_counter})
         d->release();
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -681,7 +683,8 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
     c->L = net->L;
     c->off_cubes = net->L.bytes;
     c->off_target = align16(c->off_cubes + 16u * (uint32_t)W * (uint32_t)c->H);
-    uint32_t bytes = align16(c->off_target + 16u * (uint32_t)W);
+    c->off_nodemask = align16(c->off_target + 16u * (uint32_t)W);
+    uint32_t bytes = align16(c->off_nodemask + 8u * (uint32_t)net->N);
     if (bytes > MAX_IMAGE) {
         delete c;
         return fail(PBN_E_UNSUPPORTED, "network + %d attractor cubes exceed the LDS budget", d->n_cubes);
@@ -699,6 +702,18 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
     for (int k = 0; k < W; k++) {
         tgt[k] = d->target_care[k];
         tgt[W + k] = d->target_value[k] & d->target_care[k];
+    }
+    // per node i: bit h of .x = cube h cares about i, bit h of .y = its value (first 32 cubes)
+    uint32_t* nm = reinterpret_cast<uint32_t*>(c->image.data() + c->off_nodemask);
+    for (int i = 0; i < net->N; i++) {
+        uint32_t care = 0, val = 0;
+        for (int h = 0; h < c->H && h < 32; h++) {
+            const uint64_t cw = d->cube_care[(size_t)h * W + i / 64], vw = d->cube_value[(size_t)h * W + i / 64];
+            care |= (uint32_t)((cw >> (i % 64)) & 1u) << h;
+            val |= (uint32_t)((cw & vw) >> (i % 64) & 1u) << h;
+        }
+        nm[2 * i] = care;
+        nm[2 * i + 1] = val;
     }
     c->L.bytes = bytes;
     c->reset_care.assign(d->reset_care, d->reset_care + (size_t)c->H_reset * W);
@@ -780,6 +795,9 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.L = cfg->L;
     a.off_cubes = cfg->off_cubes;
     a.off_target = cfg->off_target;
+    a.off_nodemask = cfg->off_nodemask;
+    if (int rc = b->s_counter.ensure(8)) return rc;
+    a.counter = (unsigned long long*)b->s_counter.p;
     a.n_cubes = cfg->H;
     a.B = b->B;
     a.env_base = b->env_base;
@@ -796,6 +814,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.draws_i = (const uint32_t*)d_di;
     a.draws_k = (const uint64_t*)d_dk;
     HIP_TRY(hipMemsetAsync(b->d_error, 0, 4, b->stream));
+    HIP_TRY(hipMemsetAsync(b->s_counter.p, 0, 8, b->stream));
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
     int e = launch_env_multi(b->W, a, replay, b->grid_for(b->B, bpc), b->stream);

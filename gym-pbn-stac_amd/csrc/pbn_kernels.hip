@@ -183,43 +183,113 @@ __device__ __forceinline__ bool attracting(const uint64_t (&s)[W], const uint64_
     return hit;
 }
 
+// Mismatch count of a state against one cube: #cared bits that differ from the cube.
+template <int W>
+__device__ __forceinline__ uint32_t cube_mismatch(const uint64_t (&s)[W], const uint64_t* cv) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) m += (uint32_t)__popcll((s[k] & cv[k]) ^ cv[W + k]);
+    return m;
+}
+
+template <int W, class P_t>
+__device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* cubes, int32_t H) {
+    uint64_t s[W];
+    from_plane<W>(P, s);
+    return attracting<W>(s, cubes, H);
+}
+
+// PBNTargetMultiEnv.step (pbn_target_multi.py:119-154) for every env of the batch.
+//
+// Persistent waves with lane refill: a lane that finishes its env takes the next
+// env index from a global counter (one atomic per wave per refill round), so the
+// heavy-tailed until-attractor loops (1 .. 10^4 updates) do not idle the other
+// 63 lanes of the wave. The env's state lives in the lane's LDS plane column.
+//
+// Attractor test (is_attracting_state :489-492 == "matches some cube"): for
+// H <= ENV_HMAX cubes each lane keeps, per cube, the number of cared bits that
+// differ; an update that flips node i adjusts the counters of the cubes caring
+// about i (per-node cube masks in LDS), so the test is O(H) register work per
+// update. Larger cube sets fall back to a full match after every change.
+constexpr int ENV_HMAX = 8;
+constexpr int ENV_CHUNK = 16;  // updates between refill rounds
+
 template <int W, int KIND, int REPLAY>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
+    const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     const uint32_t N = (uint32_t)a.L.n_nodes;
     const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
     const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
-    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < a.B; e += stride) {
-        uint64_t s[W];
-        load_state<W>(a.state + e * W, s);
-        const int64_t nst = a.n_steps[e] + 1;  // :123
-        bool bad = false;
-        uint64_t s_in[W];
+    const uint2* nmask = reinterpret_cast<const uint2*>(lds + a.off_nodemask);
+    const int32_t H = a.n_cubes;
+    const bool fast = H <= ENV_HMAX;
+    const uint32_t lane = __lane_id();
+
+    int64_t e = -1;
+    bool exhausted = false;
+    uint64_t o0[W];
+    uint32_t M[ENV_HMAX];
+    uint32_t used = 0;
+    int64_t nst = 0, dpos = 0, dend = 0;
+    int n_act = 0;
+    bool capped = false;
+
+    for (;;) {
+        // ---- refill idle lanes from the global work counter
+        const bool need = e < 0 && !exhausted;
+        const uint64_t need_mask = __ballot(need);
+        if (need_mask) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need_mask) - 1u;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(a.counter, (unsigned long long)__popcll(need_mask));
+            base = __shfl(base, (int)leader);
+            if (need) {
+                const uint64_t ne = base + (uint64_t)__popcll(need_mask & ((1ull << lane) - 1ull));
+                if (ne >= a.B) {
+                    exhausted = true;
+                } else {
+                    uint64_t s[W];
+                    load_state<W>(a.state + ne * W, s);
+                    bool bad = false;
+                    n_act = apply_actions<W>(s, a.actions + ne * (uint64_t)a.A, a.A, a.offset, a.dedup,
+                                             (int32_t)N, &bad);
+                    if (bad) {  // reference raises ValueError; this env is left untouched
+                        atomicOr(a.error, 1);
+                    } else {
+                        e = (int64_t)ne;
+                        nst = a.n_steps[ne] + 1;  // :123
 #pragma unroll
-        for (int k = 0; k < W; ++k) s_in[k] = s[k];
-        const int n_act = apply_actions<W>(s, a.actions + e * (uint64_t)a.A, a.A, a.offset, a.dedup, (int32_t)N, &bad);
-        if (bad) {  // reference raises ValueError; this env is left untouched
-            atomicOr(a.error, 1);
+                        for (int k = 0; k < W; ++k) o0[k] = s[k];  // :133 observation before the update
+                        to_plane<W>(P, s);
+#pragma unroll
+                        for (int h = 0; h < ENV_HMAX; ++h)
+                            M[h] = (fast && h < H) ? cube_mismatch<W>(s, cubes + (uint64_t)h * 2 * W) : 1u;
+                        used = 0;
+                        capped = false;
+                        if constexpr (REPLAY) {
+                            dpos = a.draw_off[ne];
+                            dend = a.draw_off[ne + 1];
+                        }
+                    }
+                }
+            }
+        }
+        if (__ballot(e >= 0) == 0) {
+            if (__ballot(!exhausted) == 0) break;
             continue;
         }
-        uint64_t o[W];
-#pragma unroll
-        for (int k = 0; k < W; ++k) o[k] = s[k];  // :133 observation before the update
-        (void)s_in;
-        const uint64_t g = a.env_base + e;
-        uint32_t used = 0;
-        bool capped = false;
-        int64_t dpos = 0, dend = 0;
-        if constexpr (REPLAY) {
-            dpos = a.draw_off[e];
-            dend = a.draw_off[e + 1];
-        }
-        for (;;) {
+        if (e < 0) continue;
+
+        // ---- up to ENV_CHUNK updates of this lane's env
+        const uint64_t g = a.env_base + (uint64_t)e;
+        bool done = false;
+        for (int c = 0; c < ENV_CHUNK; ++c) {
             if (used >= a.update_cap) {
                 capped = true;
+                done = true;
                 break;
             }
             uint32_t i;
@@ -227,6 +297,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             if constexpr (REPLAY) {
                 if (dpos >= dend) {
                     capped = true;
+                    done = true;
                     break;
                 }
                 i = a.draws_i[dpos];
@@ -238,22 +309,65 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 i = philox_node<KIND>(w[0], N);
                 k53 = k53_of(w[1], w[2]);
             }
-            node_update<W, KIND>(s, i, k53, lds, a.L);
+            uint32_t changed;
+            if constexpr (KIND == KIND_PREDICTOR_MIX)
+                changed = predictor_update_lds(P, i, k53, lds, a.L);
+            else
+                changed = table_update_lds(P, i, k53, lds, a.L);
             ++used;
-            // :134 the first update's result is discarded; :135-146 loop until attracting
-            if (used > 1) {
+            bool hit;
+            if (fast) {
+                // :134 the first update is never tested: the check at used == 1 is on o0
+                bool any0 = false;
 #pragma unroll
-                for (int k = 0; k < W; ++k) o[k] = s[k];
+                for (int h = 0; h < ENV_HMAX; ++h) any0 |= (h < H) && (M[h] == 0u);
+                if (used == 1 && any0) {
+                    hit = true;
+                } else {
+                    if (changed) {
+                        const uint2 m = nmask[i];
+                        const uint32_t y = P.bit(i);
+#pragma unroll
+                        for (int h = 0; h < ENV_HMAX; ++h) {
+                            const uint32_t care = (m.x >> h) & 1u, v = (m.y >> h) & 1u;
+                            M[h] = M[h] + (care ? ((y != v) ? 1u : 0xFFFFFFFFu) : 0u);
+                        }
+                    }
+                    if (used == 1) {
+                        hit = false;
+                    } else {
+                        bool z = false;
+#pragma unroll
+                        for (int h = 0; h < ENV_HMAX; ++h) z |= (h < H) && (M[h] == 0u);
+                        hit = z;
+                    }
+                }
+            } else {
+                hit = (used == 1) ? attracting<W>(o0, cubes, H)
+                                  : ((changed || used == 2) && attracting_plane<W>(P, cubes, H));
             }
-            if (attracting<W>(o, cubes, a.n_cubes)) break;
+            if (hit) {
+                done = true;
+                break;
+            }
         }
-        store_state<W>(a.state + e * W, s);
-        store_state<W>(a.obs + e * W, o);
-        a.n_steps[e] = nst;
+        if (!done) continue;
+
+        // ---- finish: outputs of step() (:148-154)
+        uint64_t s[W];
+        from_plane<W>(P, s);
+        uint64_t o[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) o[k] = used <= 1 ? o0[k] : s[k];
+        const uint64_t eu = (uint64_t)e;
+        store_state<W>(a.state + eu * W, s);
+        store_state<W>(a.obs + eu * W, o);
+        a.n_steps[eu] = nst;
         const bool term = cube_match<W>(o, target);  // :190-199 (target[0] only)
-        a.reward[e] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
-        a.flags[e] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
-        a.n_updates[e] = used;
+        a.reward[eu] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
+        a.flags[eu] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
+        a.n_updates[eu] = used;
+        e = -1;
     }
 }
 
@@ -374,7 +488,7 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay)
                                               : env_fn_w<KIND_PROB_TABLE>(W, replay);
     EnvArgs c = a;
-    return launch(fn, grid, a.L.bytes, stream, &c, sizeof c);
+    return launch(fn, grid, env_lds_bytes(W, a.L.bytes), stream, &c, sizeof c);
 }
 
 static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
@@ -394,9 +508,11 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb), blocks_per_cu);
 }
 
+uint32_t env_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK; }
+
 int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
     void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0) : env_fn_w<KIND_PROB_TABLE>(W, 0);
-    return occupancy(fn, BLOCK, lds_bytes, blocks_per_cu);
+    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes), blocks_per_cu);
 }
 
 }  // namespace pbn

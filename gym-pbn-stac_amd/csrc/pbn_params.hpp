@@ -69,6 +69,8 @@ struct EnvArgs {
     NetLayout L;
     uint32_t off_cubes;      // care/value pairs [H][2][W] u64 inside the LDS image
     uint32_t off_target;     // target care/value [2][W]
+    uint32_t off_nodemask;   // per node: {cubes caring about it, their values} as u32 bit masks
+    unsigned long long* counter;  // work-queue head (zeroed per launch)
     int32_t n_cubes;
     uint64_t B, env_base, seed;
     uint32_t call_idx, update_cap;
@@ -103,6 +105,7 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
 int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
+uint32_t env_lds_bytes(int W, uint32_t image_bytes);
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 
