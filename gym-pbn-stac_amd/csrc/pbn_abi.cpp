@@ -138,6 +138,8 @@ struct pbn_batch {
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
+    DevBuf s_ssd_hist, s_ssd_tab;                         // SSD histogram + gap/target tables
+    uint64_t ssd_iters = 0;                               // SSD iteration counter (Philox)
     // timing: mode 1 = an event pair around every launch; mode 2 = one region
     // (start before the first launch after enabling, stop after the latest launch)
     int timing = 0;
@@ -403,7 +405,7 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
-                      &b->s_counter})
+                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab})
         d->release();
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -660,6 +662,59 @@ int pbn_mt_step(pbn_batch* b, uint32_t n_updates) {
     int e = launch_mt_step(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
     if (e) return fail(PBN_E_HIP, "k_mt_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);
+}
+
+// ------------------------------------------------------------------ SSD histogram
+int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const uint32_t* flip_gap_thr,
+                uint32_t iters, uint64_t* hist) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(target_nodes, "target_nodes");
+    CHECK_NN(hist, "hist");
+    if (n_targets < 1 || n_targets > 12) return fail(PBN_E_UNSUPPORTED, "n_targets=%d outside [1, 12]", n_targets);
+    for (int j = 0; j < n_targets; j++) {
+        if (target_nodes[j] < 0 || target_nodes[j] >= b->N)
+            return fail(PBN_E_RANGE, "target node %d out of range [0, %d)", target_nodes[j], b->N);
+        for (int q = 0; q < j; q++)
+            if (target_nodes[q] == target_nodes[j]) return fail(PBN_E_INVALID, "duplicate target node %d", target_nodes[j]);
+    }
+    if (flip_gap_thr)
+        for (int k = 1; k < b->N; k++)
+            if (flip_gap_thr[k] > flip_gap_thr[k - 1]) return fail(PBN_E_INVALID, "flip_gap_thr must be non-increasing");
+    SET_DEV(b);
+    const size_t nb = (size_t)1 << n_targets;
+    if (int rc = b->s_ssd_hist.ensure(8 * nb)) return rc;
+    if (int rc = b->s_ssd_tab.ensure(4 * (size_t)b->N + 4 * (size_t)n_targets)) return rc;
+    uint32_t* d_gap = (uint32_t*)b->s_ssd_tab.p;
+    int32_t* d_tgt = (int32_t*)(d_gap + b->N);
+    if (flip_gap_thr) HIP_TRY(hipMemcpyAsync(d_gap, flip_gap_thr, 4 * (size_t)b->N, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(d_tgt, target_nodes, 4 * (size_t)n_targets, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemsetAsync(b->s_ssd_hist.p, 0, 8 * nb, b->stream));
+    SSDArgs a{};
+    a.state = b->d_state;
+    a.img = b->d_image;
+    a.L = b->net->L;
+    a.B = b->B;
+    a.env_base = b->env_base;
+    a.seed = b->seed;
+    a.iter_base = b->ssd_iters;
+    a.iters = iters;
+    a.n_targets = n_targets;
+    a.targets = d_tgt;
+    a.gap_thr = flip_gap_thr ? d_gap : nullptr;
+    a.hist = (uint64_t*)b->s_ssd_hist.p;
+    a.lds_bytes = ssd_layout(b->W, b->net->L.bytes, b->N, n_targets, &a);
+    if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "SSD LDS footprint %u B too large", a.lds_bytes);
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int e = launch_ssd(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_ssd launch: %s", hipGetErrorString((hipError_t)e));
+    if (int rc = b->ev_end(stop)) return rc;
+    std::vector<uint64_t> h(nb);
+    HIP_TRY(hipMemcpyAsync(h.data(), b->s_ssd_hist.p, 8 * nb, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    for (size_t k = 0; k < nb; k++) hist[k] += h[k];
+    b->ssd_iters += iters;
+    return 0;
 }
 
 // ------------------------------------------------------------------ R6 env

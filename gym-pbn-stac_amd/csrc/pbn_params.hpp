@@ -5,7 +5,7 @@
 namespace pbn {
 
 enum { KIND_PREDICTOR_MIX = 1, KIND_PROB_TABLE = 2 };
-enum { STREAM_STEP = 1, STREAM_INIT = 2, STREAM_ENV = 3, STREAM_RESET = 4 };
+enum { STREAM_STEP = 1, STREAM_INIT = 2, STREAM_ENV = 3, STREAM_RESET = 4, STREAM_SSD = 5, STREAM_SSD_FLIP = 6 };
 enum { STORE_FULL = 0, STORE_DIRTY = 1 };
 
 constexpr int BLOCK = 256;          // 4 wave64 per workgroup
@@ -97,7 +97,21 @@ struct MTArgs {
     uint32_t* pos_np;
 };
 
-// Launchers (pbn_kernels.hip, pbn_mt.hip). Return hipError_t as int.
+struct SSDArgs {
+    uint64_t* state;           // [B][W]
+    const void* img;           // network image
+    NetLayout L;
+    uint64_t B, env_base, seed;
+    uint64_t iter_base;        // SSD iteration counter of the first iteration (Philox c0/c1)
+    uint32_t iters;
+    int32_t n_targets;         // g <= 12 (2^g LDS bins)
+    const int32_t* targets;    // [g] node indices, first = most significant bucket bit
+    const uint32_t* gap_thr;   // [N] T_k = floor((1-p)^k 2^32), k = 1..N; null = no flips
+    uint64_t* hist;            // [2^g] accumulated counts (device)
+    uint32_t off_planes, off_gap, off_tbit, off_targets, off_hist, lds_bytes;
+};
+
+// Launchers (pbn_kernels.hip, pbn_mt.hip, pbn_ssd.hip). Return hipError_t as int.
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream);
 uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
@@ -108,5 +122,7 @@ int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes);
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
+uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a);
+int launch_ssd(int W, const SSDArgs& a, int grid, void* stream);
 
 }  // namespace pbn

@@ -141,6 +141,21 @@ class EnvConfig:
             self._h = None
 
 
+def flip_gap_table(n_nodes: int, p: float):
+    """Geometric-gap thresholds for independent Bernoulli(p) node flips.
+
+    ``T_k = floor((1-p)^k * 2^32)`` for k = 1..N, so that a 32-bit uniform u gives
+    ``gap = #{k >= 1 : u < T_k}`` with ``P(gap >= k) = (1-p)^k``. ``None`` for p == 0.
+    """
+    if not (0.0 <= p <= 1.0):
+        raise ValueError("Invalid Bit Flip Probability value.")  # eval.py:32-34
+    if p == 0.0:
+        return None
+    k = np.arange(1, n_nodes + 1, dtype=np.float64)
+    t = np.floor(np.power(1.0 - p, k) * 4294967296.0)
+    return np.minimum(t, 4294967295.0).astype(np.uint32)
+
+
 def cube_arrays(cubes: Sequence, n_nodes: int):
     """Hypercube tuples (ints / '*') -> (care, value) [H][W] uint64."""
     W = (n_nodes + 63) // 64
@@ -294,6 +309,16 @@ class PBNBatch:
                                                 int(bool(dedup)), int(offset), int(update_cap),
                                                 C.c_void_p(d_obs), C.c_void_p(d_reward), C.c_void_p(d_flags),
                                                 C.c_void_p(d_n_updates)))
+
+    # -- SSD histogram (utils/eval.py:20-103) -------------------------------
+    def ssd_counts(self, target_nodes, iters: int, bit_flip_prob: float = 0.01) -> np.ndarray:
+        """Run ``iters`` SSD iterations on every env; returns counts [2^g] (first target = MSB)."""
+        t = np.ascontiguousarray(target_nodes, dtype=np.int32)
+        gap = flip_gap_table(self.n_nodes, bit_flip_prob)
+        hist = np.zeros(1 << t.size, dtype=np.uint64)
+        L.check(L.lib.pbn_ssd_run(self._h, L.ptr(t, L._i32p), int(t.size), L.ptr(gap, L._u32p), int(iters),
+                                  L.ptr(hist, L._u64p)))
+        return hist
 
     # -- timing -----------------------------------------------------------
     def timing(self, mode):

@@ -170,6 +170,13 @@ int pbn_env_step_multi_replay(pbn_batch *b, const pbn_envcfg *cfg, const int32_t
                               const uint64_t *draws_k, uint64_t *obs, int32_t *reward, uint8_t *flags,
                               uint32_t *n_updates);
 
+/* ---- steady-state distribution: compute_ssd_hist / _ssd_run (gym_PBN/utils/eval.py:20-103) ----
+ * Every env runs `iters` iterations of: count the bucket of target_nodes (first = MSB), flip each
+ * node with probability p, one async transition (Philox). flip_gap_thr [N]: T_k = floor((1-p)^k 2^32),
+ * k = 1..N (NULL: no flips). hist [2^n_targets] host counts, ACCUMULATED (+=). n_targets <= 12. */
+int pbn_ssd_run(pbn_batch *b, const int32_t *target_nodes, int n_targets, const uint32_t *flip_gap_thr,
+                uint32_t iters, uint64_t *hist);
+
 /* ---- measurement: HIP events on the batch stream. mode 1: a pair around every kernel launch;
  *      mode 2: one region from before the first launch to after the last (launch gaps included) ---- */
 int pbn_timing_enable(pbn_batch *b, int enable);

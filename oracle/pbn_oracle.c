@@ -467,3 +467,45 @@ EXPORT void orc_env_reset_philox(const orc_net *n, uint64_t *state, int64_t *n_s
         n_steps[e] = 0;
     }
 }
+
+/* compute_ssd_hist / _ssd_run (gym_PBN/utils/eval.py:76-103), Philox mode, same streams and
+ * geometric-gap flip procedure as the kernel; the bucket is recomputed from the state every
+ * iteration (not incrementally), as the reference does via getTargetIdx(). */
+enum { STREAM_SSD = 5, STREAM_SSD_FLIP = 6 };
+
+EXPORT int orc_ssd_philox(const orc_net *n, uint64_t *state, int64_t B, const int32_t *targets, int g,
+                          const uint32_t *gap_thr, uint64_t seed, uint64_t env_base, uint64_t iter_base,
+                          uint32_t iters, uint64_t *hist) {
+    const int W = n->n_words, N = n->n_nodes;
+    for (int64_t e = 0; e < B; e++) {
+        uint64_t *s = state + e * W;
+        uint64_t gid = env_base + (uint64_t)e;
+        for (uint32_t t = 0; t < iters; t++) {
+            uint64_t it = iter_base + t;
+            uint32_t bucket = 0;
+            for (int j = 0; j < g; j++) bucket = (bucket << 1) | (uint32_t)getbit(s, targets[j]);
+            hist[bucket]++;
+            if (gap_thr) {
+                uint32_t w[4];
+                uint32_t m = 0, wi = 4, pos = 0;
+                int first = 1;
+                for (;;) {
+                    if (wi == 4) {
+                        philox_draw(seed, (uint32_t)it, m++, gid, STREAM_SSD_FLIP, w);
+                        wi = 0;
+                    }
+                    uint32_t u = w[wi++], gap = 0;
+                    while (gap < (uint32_t)N && u < gap_thr[gap]) gap++; /* #{k>=1 : u < T_k} */
+                    pos = first ? gap : pos + 1u + gap;
+                    first = 0;
+                    if (pos >= (uint32_t)N) break;
+                    setbit(s, (int)pos, !getbit(s, (int)pos));
+                }
+            }
+            uint32_t w[4];
+            philox_draw(seed, (uint32_t)it, (uint32_t)(it >> 32), gid, STREAM_SSD, w);
+            node_update(n, s, philox_node(n, w[0]), philox_k53(w));
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,73 @@
+"""SSD histogram (utils/eval.py:20-103): flip process statistics (CPU) and device parity (GPU)."""
+
+import numpy as np
+import pytest
+
+from gym_pbn_amd.network import load_network
+
+
+def _gap_positions(u_stream, T, N):
+    """The kernel/oracle flip procedure: successive gaps = #{k>=1 : u < T_k}."""
+    out, pos, first = [], 0, True
+    for u in u_stream:
+        gap = int(np.searchsorted(-T.astype(np.int64), -int(u), side="right"))  # #{k : T_k > u}
+        pos = gap if first else pos + 1 + gap
+        first = False
+        if pos >= N:
+            return out
+        out.append(pos)
+    raise AssertionError("stream exhausted")
+
+
+def test_flip_gap_table_is_bernoulli_process():
+    from gym_pbn_amd.batch import flip_gap_table
+
+    N, p, R = 40, 0.05, 40000
+    T = flip_gap_table(N, p)
+    assert T.shape == (N,) and np.all(np.diff(T.astype(np.int64)) <= 0)
+    rng = np.random.default_rng(0)
+    counts = np.zeros(N)
+    pair = 0
+    for _ in range(R):
+        pos = _gap_positions(rng.integers(0, 2**32, size=64, dtype=np.uint64), T, N)
+        counts[pos] += 1
+        pair += (3 in pos) and (17 in pos)
+    # each node flips with probability p, independently
+    assert np.all(np.abs(counts / R - p) < 5 * np.sqrt(p * (1 - p) / R))
+    assert abs(pair / R - p * p) < 5 * np.sqrt(p * p / R)
+    assert flip_gap_table(N, 0.0) is None
+    assert np.all(flip_gap_table(N, 1.0) == 0)
+
+
+GPU_CASES = [("bittner28", [0, 1, 2, 3, 6, 7, 9], 3000, 0.01), ("bittner199", [0, 1, 2, 3, 4, 5, 6], 2000, 0.01),
+             ("tt200", [5, 50, 150], 1500, 0.02), ("bittner70", [1, 2], 1000, 0.0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,targets,iters,p", GPU_CASES)
+def test_ssd_matches_oracle(oracle_mod, name, targets, iters, p):
+    from gym_pbn_amd.batch import PBNBatch, flip_gap_table
+
+    net = load_network(name)
+    B = 600
+    b = PBNBatch(net, B, seed=17, env_id_base=5)
+    b.randomize()
+    s0 = b.get_state()
+    h1 = b.ssd_counts(targets, iters, p)
+    h2 = b.ssd_counts(targets, iters // 2, p)  # continues the iteration counter
+    o = oracle_mod.Oracle(net)
+    gap = flip_gap_table(net.n_nodes, p)
+    st, r1 = oracle_mod.ssd_philox(o, s0, targets, gap, 17, 5, 0, iters)
+    st, r2 = oracle_mod.ssd_philox(o, st, targets, gap, 17, 5, iters, iters // 2)
+    assert np.array_equal(h1, r1) and np.array_equal(h2, r2)
+    assert np.array_equal(b.get_state(), st)
+    assert int(h1.sum()) == B * iters
+
+
+@pytest.mark.gpu
+def test_compute_ssd_hist_normalised():
+    from gym_pbn_amd.eval import compute_ssd_hist
+
+    df = compute_ssd_hist("bittner28", [0, 1, 2, 3, 6, 7, 9], iters=120_000, resets=300, seed=3)
+    assert list(df.index[:2]) == ["0000000", "0000001"] and len(df) == 128
+    assert abs(df["Value"].sum() - 1.0) < 1e-9
