@@ -140,6 +140,8 @@ struct pbn_batch {
     DevBuf s_counter;                                     // env-step work-queue head
     DevBuf s_ssd_hist, s_ssd_tab;                         // SSD histogram + gap/target tables
     uint64_t ssd_iters = 0;                               // SSD iteration counter (Philox)
+    DevBuf s_sync_tab;                                    // perturbation gap table
+    uint64_t sync_steps = 0;                              // synchronous-step counter (Philox)
     // timing: mode 1 = an event pair around every launch; mode 2 = one region
     // (start before the first launch after enabling, stop after the latest launch)
     int timing = 0;
@@ -405,7 +407,7 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
-                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab})
+                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab})
         d->release();
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -662,6 +664,42 @@ int pbn_mt_step(pbn_batch* b, uint32_t n_updates) {
     int e = launch_mt_step(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
     if (e) return fail(PBN_E_HIP, "k_mt_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);
+}
+
+// ------------------------------------------------------------------ synchronous update
+int pbn_synch_step(pbn_batch* b, uint32_t n_steps, const uint32_t* perturb_gap_thr) {
+    CHECK_NN(b, "batch");
+    if (!n_steps) return 0;
+    if (perturb_gap_thr)
+        for (int k = 1; k < b->N; k++)
+            if (perturb_gap_thr[k] > perturb_gap_thr[k - 1])
+                return fail(PBN_E_INVALID, "perturb_gap_thr must be non-increasing");
+    SET_DEV(b);
+    SyncArgs a{};
+    a.state = b->d_state;
+    a.img = b->d_image;
+    a.L = b->net->L;
+    a.B = b->B;
+    a.env_base = b->env_base;
+    a.seed = b->seed;
+    a.step_base = b->sync_steps;
+    a.T = n_steps;
+    if (perturb_gap_thr) {
+        if (int rc = b->s_sync_tab.ensure(4 * (size_t)b->N)) return rc;
+        HIP_TRY(hipMemcpyAsync(b->s_sync_tab.p, perturb_gap_thr, 4 * (size_t)b->N, hipMemcpyHostToDevice,
+                               b->stream));
+        a.gap_thr = (const uint32_t*)b->s_sync_tab.p;
+    }
+    a.lds_bytes = sync_layout(b->W, b->net->L.bytes, b->N, &a);
+    if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "sync LDS footprint %u B too large", a.lds_bytes);
+    hipEvent_t stop;
+    if (int rc = b->ev_begin(&stop)) return rc;
+    int e = launch_sync(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_sync launch: %s", hipGetErrorString((hipError_t)e));
+    if (int rc = b->ev_end(stop)) return rc;
+    b->sync_steps += n_steps;
+    if (perturb_gap_thr) HIP_TRY(hipStreamSynchronize(b->stream));  // table buffer is reused by later calls
+    return 0;
 }
 
 // ------------------------------------------------------------------ SSD histogram

@@ -195,10 +195,11 @@ struct PlaneT {
 };
 using Plane = PlaneT<BLOCK>;
 
-// Bittner Predstep (base.py:89-119) on the LDS plane; returns 1 if the bit changed.
+// Bittner Predstep (base.py:89-119) evaluated on the LDS plane: the new value of node i.
+// `self` is the dword holding node i (already read by the caller).
 template <class P_t>
-__device__ __forceinline__ uint32_t predictor_update_lds(const P_t& P, uint32_t i, uint64_t k53,
-                                                         const uint8_t* tbl, const NetLayout& L) {
+__device__ __forceinline__ uint32_t predictor_eval_lds(const P_t& P, uint32_t i, uint32_t self, uint64_t k53,
+                                                       const uint8_t* tbl, const NetLayout& L) {
     const uint32_t info = reinterpret_cast<const uint32_t*>(tbl + L.off_node)[i];
     const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
     const uint64_t* thr = reinterpret_cast<const uint64_t*>(tbl + L.off_thr) + o0;
@@ -206,20 +207,15 @@ __device__ __forceinline__ uint32_t predictor_update_lds(const P_t& P, uint32_t 
 #pragma unroll 4
     for (uint32_t q = 0; q + 1 < cnt; ++q) j += (k53 >= thr[q]) ? 1u : 0u;
     const uint64_t rec = reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[o0 + j];
-    const uint32_t d = i >> 5, sh = i & 31u;
-    const uint32_t self = P.get(d);
     const uint32_t p = (P.bit((uint32_t)rec & 0xFFFFu) << 3) | (P.bit((uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
-                       (P.bit((uint32_t)(rec >> 32) & 0xFFFFu) << 1) | ((self >> sh) & 1u);
-    const uint32_t y = (uint32_t)(rec >> (48 + p)) & 1u;
-    const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-    P.put(d, nv);
-    return nv != self;
+                       (P.bit((uint32_t)(rec >> 32) & 0xFFFFu) << 1) | ((self >> (i & 31u)) & 1u);
+    return (uint32_t)(rec >> (48 + p)) & 1u;
 }
 
-// PBN node update (common/node.py:31-38) on the LDS plane.
+// PBN Node.compute_next_value (common/node.py:31-38) evaluated on the LDS plane.
 template <class P_t>
-__device__ __forceinline__ uint32_t table_update_lds(const P_t& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
-                                                     const NetLayout& L) {
+__device__ __forceinline__ uint32_t table_eval_lds(const P_t& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
+                                                   const NetLayout& L) {
     const uint64_t info = reinterpret_cast<const uint64_t*>(tbl + L.off_node)[i];
     const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu, k = (uint32_t)(info >> 48) & 0xFFu;
     const uint16_t* in = reinterpret_cast<const uint16_t*>(tbl + L.off_rec) + ioff;
@@ -227,12 +223,61 @@ __device__ __forceinline__ uint32_t table_update_lds(const P_t& P, uint32_t i, u
 #pragma unroll 4
     for (uint32_t q = 0; q < k; ++q) idx = (idx << 1) | P.bit(in[q]);
     const uint64_t t = reinterpret_cast<const uint64_t*>(tbl + L.off_thr)[toff + idx];
-    const uint32_t y = k53 < t ? 1u : 0u;
+    return k53 < t ? 1u : 0u;
+}
+
+// Async update of node i in place on the plane; returns 1 if the bit changed.
+template <class P_t>
+__device__ __forceinline__ uint32_t predictor_update_lds(const P_t& P, uint32_t i, uint64_t k53,
+                                                         const uint8_t* tbl, const NetLayout& L) {
+    const uint32_t d = i >> 5, sh = i & 31u;
+    const uint32_t self = P.get(d);
+    const uint32_t y = predictor_eval_lds(P, i, self, k53, tbl, L);
+    const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+    P.put(d, nv);
+    return nv != self;
+}
+
+template <class P_t>
+__device__ __forceinline__ uint32_t table_update_lds(const P_t& P, uint32_t i, uint64_t k53, const uint8_t* tbl,
+                                                     const NetLayout& L) {
+    const uint32_t y = table_eval_lds(P, i, k53, tbl, L);
     const uint32_t d = i >> 5, sh = i & 31u;
     const uint32_t self = P.get(d);
     const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
     P.put(d, nv);
     return nv != self;
+}
+
+// Independent Bernoulli(p) events over positions [0, N) generated as successive
+// geometric gaps: gap = #{k >= 1 : u < T_k}, T_k = floor((1-p)^k 2^32) (LDS table
+// gap[0..N-1] = T_1..T_N), u = 32-bit Philox words from ctr {c0, m, gid, stream}
+// with m = 0, 1, ... Calls on_pos(pos) for every event position in increasing order.
+template <class F>
+__device__ __forceinline__ void bernoulli_positions(uint64_t seed, uint32_t c0, uint32_t stream, uint64_t gid,
+                                                    const uint32_t* gap, uint32_t N, F&& on_pos) {
+    uint32_t w[4];
+    uint32_t m = 0, wi = 4, pos = 0;
+    bool first = true;
+    for (;;) {
+        if (wi == 4) {
+            philox_draw(seed, c0, m++, gid, stream, w);
+            wi = 0;
+        }
+        const uint32_t u = w[wi++];
+        uint32_t lo = 0, hi = N;  // largest k in [0, N] with u < T_k (T_0 = +inf)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (u < gap[mid - 1])
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        pos = first ? lo : pos + 1u + lo;
+        first = false;
+        if (pos >= N) break;
+        on_pos(pos);
+    }
 }
 
 template <int W, class P_t>

@@ -5,7 +5,16 @@
 namespace pbn {
 
 enum { KIND_PREDICTOR_MIX = 1, KIND_PROB_TABLE = 2 };
-enum { STREAM_STEP = 1, STREAM_INIT = 2, STREAM_ENV = 3, STREAM_RESET = 4, STREAM_SSD = 5, STREAM_SSD_FLIP = 6 };
+enum {
+    STREAM_STEP = 1,
+    STREAM_INIT = 2,
+    STREAM_ENV = 3,
+    STREAM_RESET = 4,
+    STREAM_SSD = 5,
+    STREAM_SSD_FLIP = 6,
+    STREAM_SYNC = 7,
+    STREAM_SYNC_PERT = 8
+};
 enum { STORE_FULL = 0, STORE_DIRTY = 1 };
 
 constexpr int BLOCK = 256;          // 4 wave64 per workgroup
@@ -111,7 +120,18 @@ struct SSDArgs {
     uint32_t off_planes, off_gap, off_tbit, off_targets, off_hist, lds_bytes;
 };
 
-// Launchers (pbn_kernels.hip, pbn_mt.hip, pbn_ssd.hip). Return hipError_t as int.
+struct SyncArgs {
+    uint64_t* state;          // [B][W]
+    const void* img;          // network image
+    NetLayout L;
+    uint64_t B, env_base, seed;
+    uint64_t step_base;       // synchronous-step counter of the first step (Philox)
+    uint32_t T;
+    const uint32_t* gap_thr;  // [N] perturbation gap table (T_k = floor((1-p)^k 2^32)); null = off
+    uint32_t off_planes, off_gap, lds_bytes;
+};
+
+// Launchers (pbn_kernels.hip, pbn_mt.hip, pbn_ssd.hip, pbn_sync.hip). Return hipError_t as int.
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream);
 uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
@@ -124,5 +144,7 @@ int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a);
 int launch_ssd(int W, const SSDArgs& a, int grid, void* stream);
+uint32_t sync_layout(int W, uint32_t image_bytes, int n_nodes, SyncArgs* a);
+int launch_sync(int W, const SyncArgs& a, int grid, void* stream);
 
 }  // namespace pbn

@@ -61,33 +61,13 @@ __global__ __launch_bounds__(BLOCK) void k_ssd(SSDArgs a) {
             }
             ++run;
             // independent Bernoulli(p) flips (eval.py:92-95) as geometric gaps
-            if (a.gap_thr) {
-                uint32_t w[4];
-                uint32_t m = 0, wi = 4, pos = 0;
-                bool first = true;
-                for (;;) {
-                    if (wi == 4) {
-                        philox_draw(a.seed, (uint32_t)it, m++, g, STREAM_SSD_FLIP, w);
-                        wi = 0;
-                    }
-                    const uint32_t u = w[wi++];
-                    uint32_t lo = 0, hi = N;  // largest k in [0, N] with u < T_k (T_0 = +inf)
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi + 1) >> 1;
-                        if (u < gap[mid - 1])
-                            lo = mid;
-                        else
-                            hi = mid - 1;
-                    }
-                    pos = first ? lo : pos + 1u + lo;
-                    first = false;
-                    if (pos >= N) break;
+            if (a.gap_thr)
+                bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, [&](uint32_t pos) {
                     const uint32_t d = pos >> 5, sh = pos & 31u;
                     P.put(d, P.get(d) ^ (1u << sh));
                     const int tb = tbit[pos];
                     if (tb >= 0) bucket ^= 1u << tb;
-                }
-            }
+                });
             // one transition (env.step(action=0), eval.py:96)
             uint32_t w[4];
             philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);

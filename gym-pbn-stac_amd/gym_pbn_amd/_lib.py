@@ -110,6 +110,7 @@ SIGNATURES = {
     "pbn_env_step_multi_replay": (C.c_int, [_vp, _vp, _i32p, C.c_int, C.c_int, C.c_int, _i64p, _u32p, _u64p, _u64p,
                                             _i32p, _u8p, _u32p]),
     "pbn_ssd_run": (C.c_int, [_vp, _i32p, C.c_int, _u32p, C.c_uint32, _u64p]),
+    "pbn_synch_step": (C.c_int, [_vp, C.c_uint32, _u32p]),
     "pbn_timing_enable": (C.c_int, [_vp, C.c_int]),
     "pbn_timing_read": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
 }

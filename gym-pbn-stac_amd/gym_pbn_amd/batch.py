@@ -310,6 +310,11 @@ class PBNBatch:
                                                 C.c_void_p(d_obs), C.c_void_p(d_reward), C.c_void_p(d_flags),
                                                 C.c_void_p(d_n_updates)))
 
+    def synch_step(self, n_steps: int = 1, perturbation_prob: float = 0.0):
+        """Synchronous update (base.py:286-303); perturbation_prob > 0 enables perturbations (p=0.001 there)."""
+        gap = flip_gap_table(self.n_nodes, perturbation_prob)
+        L.check(L.lib.pbn_synch_step(self._h, int(n_steps), L.ptr(gap, L._u32p)))
+
     # -- SSD histogram (utils/eval.py:20-103) -------------------------------
     def ssd_counts(self, target_nodes, iters: int, bit_flip_prob: float = 0.01) -> np.ndarray:
         """Run ``iters`` SSD iterations on every env; returns counts [2^g] (first target = MSB)."""

@@ -170,6 +170,12 @@ int pbn_env_step_multi_replay(pbn_batch *b, const pbn_envcfg *cfg, const int32_t
                               const uint64_t *draws_k, uint64_t *obs, int32_t *reward, uint8_t *flags,
                               uint32_t *n_updates);
 
+/* ---- synchronous update: Graph.synch_step (base.py:286-303), Philox mode ----
+ * every node from the pre-step snapshot, each with its own random(); perturb_gap_thr [N]
+ * (T_k = floor((1-p)^k 2^32), NULL = perturbations off): if any node is perturbed, the
+ * perturbed nodes flip and no update happens in that step (base.py:288-295). */
+int pbn_synch_step(pbn_batch *b, uint32_t n_steps, const uint32_t *perturb_gap_thr);
+
 /* ---- steady-state distribution: compute_ssd_hist / _ssd_run (gym_PBN/utils/eval.py:20-103) ----
  * Every env runs `iters` iterations of: count the bucket of target_nodes (first = MSB), flip each
  * node with probability p, one async transition (Philox). flip_gap_thr [N]: T_k = floor((1-p)^k 2^32),

@@ -509,3 +509,60 @@ EXPORT int orc_ssd_philox(const orc_net *n, uint64_t *state, int64_t B, const in
     }
     return 0;
 }
+
+/* Graph.synch_step (base.py:286-303), Philox mode: perturbation flags via the geometric-gap
+ * procedure (any flag -> flip flagged nodes, no update); otherwise every node from the snapshot,
+ * node i's random() from philox(seed, {step_lo, (i>>1) | step_hi<<16, gid, SYNC}) words
+ * (0,1) for even i and (2,3) for odd i. Probability-table networks update node 0 too. */
+enum { STREAM_SYNC = 7, STREAM_SYNC_PERT = 8 };
+
+static inline uint32_t geo_gap(uint32_t u, const uint32_t *gap, int N) {
+    uint32_t k = 0;
+    while (k < (uint32_t)N && u < gap[k]) k++;
+    return k;
+}
+
+EXPORT int orc_sync_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_t seed, uint64_t env_base,
+                           uint64_t step_base, uint32_t T, const uint32_t *gap_thr) {
+    const int W = n->n_words, N = n->n_nodes;
+    for (int64_t e = 0; e < B; e++) {
+        uint64_t *s = state + e * W;
+        uint64_t gid = env_base + (uint64_t)e;
+        for (uint32_t t = 0; t < T; t++) {
+            uint64_t st = step_base + t;
+            int flipped = 0;
+            if (gap_thr) {
+                uint32_t w[4], m = 0, wi = 4, pos = 0;
+                int first = 1;
+                for (;;) {
+                    if (wi == 4) {
+                        philox_draw(seed, (uint32_t)st, m++, gid, STREAM_SYNC_PERT, w);
+                        wi = 0;
+                    }
+                    uint32_t gp = geo_gap(w[wi++], gap_thr, N);
+                    pos = first ? gp : pos + 1u + gp;
+                    first = 0;
+                    if (pos >= (uint32_t)N) break;
+                    setbit(s, (int)pos, !getbit(s, (int)pos));
+                    flipped = 1;
+                }
+            }
+            if (flipped) continue;
+            uint64_t old[64], nxt[64];
+            memcpy(old, s, 8 * (size_t)W);
+            memcpy(nxt, s, 8 * (size_t)W);
+            uint32_t w[4];
+            for (int i = 0; i < N; i++) {
+                if ((i & 1) == 0)
+                    philox_draw(seed, (uint32_t)st, ((uint32_t)i >> 1) | ((uint32_t)(st >> 32) << 16), gid,
+                                STREAM_SYNC, w);
+                uint64_t k53 = (i & 1) ? (((uint64_t)(w[2] >> 5) << 26) | (w[3] >> 6))
+                                       : (((uint64_t)(w[0] >> 5) << 26) | (w[1] >> 6));
+                int y = n->kind == 1 ? predstep(n, old, i, k53) : ttstep(n, old, i, k53);
+                setbit(nxt, i, y);
+            }
+            memcpy(s, nxt, 8 * (size_t)W);
+        }
+    }
+    return 0;
+}
