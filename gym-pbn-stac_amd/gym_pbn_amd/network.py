@@ -288,6 +288,13 @@ class TruthTableNetwork:
             name=name,
         )
 
+    @classmethod
+    def from_logic_funcs(cls, nodes: Sequence[str], node_functions: Sequence, name: str = "pbn"):
+        """``PBN(logic_func_data=(nodes, node_functions))`` (``common/pbn.py:47-51``, ``converters.py:9-40``)."""
+        from .io.logic import logic_funcs_to_pbn_data
+
+        return cls.from_pbn_data(logic_funcs_to_pbn_data(nodes, node_functions), name=name)
+
     def save(self, path) -> None:
         np.savez_compressed(
             path, kind=np.int32(self.kind), name=np.array(self.name), node_k=self.node_k,

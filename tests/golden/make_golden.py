@@ -321,6 +321,168 @@ def gen_cabean_kat(multi):
     print("cabean kat", doc["expected"])
 
 
+LOGIC_EXPRS = [
+    "(a)", "(a and b)", "((a or b) and c)", "not not a", "a and not b or c", "True", "False", "a or True and b",
+    "not (a or b)", "(not a)", "a and (b or (c and d))", "x1 and x2", "a and", "and a", "a b", "((a)", "a))",
+    "not a and b", "a or b and c", "True or a", "a and True", "True and a", "not True", "(True)", "gene_1 and x",
+    "a1b2 and c", "(a or b) and (c or d)", "not", "a or", ")", "( a )", "not (a and (b or not c)) or d and not a",
+    "a and b or c and d or not e", "((a and b))", "(a or (b))", "a not b", "a (b)", "1a", "a or not (b and c)",
+    "not a or not b and not c", "(a or b) and not (c or d) or (e and not a)", "False or a", "a and False",
+]
+LOGIC_NETS = [
+    (["u", "x1", "x2", "x3", "x4"],  # example.py:24-35 (test_example_1)
+     [[], [("not x2 and not x4", 1)], [("not x4 and not u and (x2 or x3)", 1)],
+      [("not x2 and not x4 and x1", 0.7), ("False", 0.3)], [("not x2 and not x3", 1)]]),
+    (["a", "b", "c", "d"],
+     [[("b or c", 0.25), ("not d", 0.35), ("b and c and d", 0.4)], [("True", 0.5), ("a", 0.5)],
+      [("(a or b) and (d or a)", 0.1), ("not a", 0.2), ("b", 0.3), ("d", 0.15)], [("a and b and c", 1)]]),
+    (["p", "q"], [[("q", 0.3)], [("p", 0.1), ("p", 0.2), ("not p", 0.7)]]),
+    (["a", "b"], [[("c", 1)], [("a", 1)]]),  # unknown symbol
+]
+
+
+def gen_logic():
+    """Logic evaluator + converter KATs (utils/logic/eval.py, utils/converters.py:9-40)."""
+    ev = sys.modules["gym_PBN.utils.logic.eval"]
+    conv = sys.modules["gym_PBN.utils.converters"]
+    exprs = []
+    for e in LOGIC_EXPRS:
+        rec = {"expr": e}
+        try:
+            syms = ev.LogicExpressionEvaluator.get_symbols(e)
+            rec["symbols"] = syms
+            order = sorted(set(syms))
+            vals = []
+            for bits in product([0, 1], repeat=len(order)):
+                vals.append(int(ev.LogicExpressionEvaluator(dict(zip(order, bits))).evaluate(e)))
+            rec["values"] = vals
+        except Exception as exc:  # the reference rejects it
+            rec["error"] = type(exc).__name__
+        exprs.append(rec)
+    nets = []
+    for nodes, funcs in LOGIC_NETS:
+        rec = {"nodes": nodes, "functions": [[list(f) for f in fs] for fs in funcs]}
+        try:
+            data = conv.logic_funcs_to_PBN_data(nodes, funcs)
+            rec["expected"] = [{"mask": [int(x) for x in d[0]], "table": np.asarray(d[1]).reshape(-1).tolist(),
+                                "name": d[2], "control": bool(d[3])} for d in data]
+        except Exception as exc:
+            rec["error"] = type(exc).__name__
+        nets.append(rec)
+    (HERE / "logic_kat.json").write_text(json.dumps({"expressions": exprs, "networks": nets}, indent=1) + "\n")
+    print("logic kat", sum("error" in r for r in exprs), "rejected of", len(exprs))
+
+
+def _mdp_networks():
+    """(name, PBN_data or None, logic_func_data or None) used for the env fixtures.
+
+    ``PBNEnv.reset`` loops until it draws an attractor of at most 10 states
+    (``pbn_env.py:204-206``), so every network here has one.
+    """
+    rng = np.random.default_rng(35)
+    data = []
+    N = 6
+    for i in range(N):
+        others = [j for j in range(N) if j != i]
+        k = 2 if i else 0  # node 0: no inputs -> a control node for the PBCN envs
+        inp = sorted(rng.choice(others, size=k, replace=False).tolist())
+        mask = np.zeros(N, dtype=bool)
+        mask[inp] = True
+        tt = rng.choice([0.0, 1.0, 0.0, 1.0, 0.8], size=(2,) * k) if k else np.array(0.0)
+        data.append((mask, tt, f"G{i}", k == 0))
+    logic4 = (["u", "a", "b", "c"], [[], [("not b", 1)], [("a and not u", 1)], [("b or c", 0.5), ("a", 0.5)]])
+    return [("tt6", data, None), ("logic5", None, LOGIC_NETS[0]), ("logic4", None, logic4)]
+
+
+def _to_json_data(data):
+    return [{"mask": [int(x) for x in d[0]], "table": np.asarray(d[1]).reshape(-1).tolist(), "name": d[2],
+             "control": bool(d[3])} for d in data]
+
+
+def gen_mdp(node_mod, pbn_mod):
+    """R7 + macro-action env KATs: PBNEnv, PBCNEnv, sampled-data and self-triggering envs.
+
+    Each env is the reference class itself (gymnasium spaces are inert stand-ins whose
+    ``contains`` accepts everything; only valid actions are fed). Transition draws
+    (stdlib ``randint``, numpy ``uniform``) and the self-triggering termination draws
+    (stdlib ``uniform``) are logged per env step so the device envs can replay them;
+    ``reset(seed)``'s own ``random.choice`` draws are not replayed -- the device env
+    must reproduce the reset state from the seed.
+    """
+    import contextlib
+    import io
+    pbn_env, pbcn_env, sampled, selftrig, pbcn = refload.load_mdp_envs()
+    kinds = [("PBNEnv", pbn_env.PBNEnv, {}), ("PBNSampledDataEnv", sampled.PBNSampledDataEnv, {"T": 4}),
+             ("PBNSelfTriggeringEnv", selftrig.PBNSelfTriggeringEnv, {}), ("PBCNEnv", pbcn_env.PBCNEnv, {}),
+             ("PBCNSampledDataEnv", sampled.PBCNSampledDataEnv, {"T": 3}),
+             ("PBCNSelfTriggeringEnv", selftrig.PBCNSelfTriggeringEnv, {"T": 6})]
+    rec_std, rec_np, rec_st = (refload.DrawRecorder(random), refload.DrawRecorder(np.random),
+                               refload.DrawRecorder(random))
+    out = []
+    for net_name, data, logic in _mdp_networks():
+        src = {"PBN_data": list(data) if data is not None else [], "logic_func_data": logic}
+        with contextlib.redirect_stdout(io.StringIO()):
+            probe = pbn_env.PBNEnv(goal_config={"all_attractors": [], "target_nodes": set()}, **src)
+        attractors = [list(a) for a in probe.all_attractors]
+        target = {attractors[-1][0]}
+        rng = np.random.default_rng(11)
+        for kind, cls, extra in kinds:
+            with contextlib.redirect_stdout(io.StringIO()):
+                env = cls(goal_config={"all_attractors": [], "target_nodes": set(target)}, **src, **extra)
+            N = env.PBN.N
+            M = getattr(env.PBN, "M", 0)
+            rec = {"network": net_name, "kind": kind, "extra": extra, "attractors": [[list(s) for s in a]
+                                                                                    for a in attractors],
+                   "target": [list(t) for t in target], "episodes": []}
+            pbn_mod.random, pbcn.randint, node_mod.random, selftrig.random = (rec_std, rec_std.randint, rec_np,
+                                                                              rec_st)
+            try:
+                for seed in (0, 1, 2, 5, 9):
+                    ep = {"seed": seed}
+                    try:
+                        with contextlib.redirect_stdout(io.StringIO()):
+                            obs, info = env.reset(seed=seed)
+                    except ValueError:
+                        ep["reset_error"] = True
+                        rec["episodes"].append(ep)
+                        continue
+                    ep["reset_obs"] = [int(x) for x in obs]
+                    steps = []
+                    for t in range(12):
+                        if kind == "PBNEnv" or kind == "PBCNEnv":
+                            a = int(rng.integers(0, N)) if rng.random() < 0.6 else 0
+                        elif kind == "PBNSampledDataEnv":
+                            a = (int(rng.integers(0, N + 1)), int(rng.integers(1, 5)))
+                        elif kind == "PBNSelfTriggeringEnv":
+                            a = (int(rng.integers(0, N + 1)), int(rng.integers(1, 11)))
+                        elif kind == "PBCNSampledDataEnv":
+                            a = int(rng.integers(0, (2 ** M) * 3))
+                        else:
+                            a = int(rng.integers(0, (2 ** M) * 10))
+                        for r in (rec_std, rec_np, rec_st):
+                            r.log.clear()
+                        with contextlib.redirect_stdout(io.StringIO()):
+                            o, reward, term, trunc, info = env.step(a)
+                        assert all(e[0] == "i" for e in rec_std.log) and len(rec_std.log) == len(rec_np.log)
+                        steps.append({"action": list(a) if isinstance(a, tuple) else a,
+                                      "obs": [int(x) for x in o], "reward": reward, "terminated": bool(term),
+                                      "truncated": bool(trunc), "interval": info.get("interval"),
+                                      "observation_idx": int(info["observation_idx"]),
+                                      "node_idx": [int(e[1]) for e in rec_std.log],
+                                      "k53": [k53_of(e[1]) for e in rec_np.log],
+                                      "term_u": [float(e[1]) for e in rec_st.log]})
+                    ep["steps"] = steps
+                    rec["episodes"].append(ep)
+            finally:
+                pbn_mod.random, pbcn.randint, node_mod.random, selftrig.random = (random, random.randint, np.random,
+                                                                                  random)
+            out.append(rec)
+    nets = {n: {"PBN_data": _to_json_data(d) if d is not None else None, "logic_func_data": lf}
+            for n, d, lf in _mdp_networks()}
+    (HERE / "mdp_kat.json").write_text(json.dumps({"networks": nets, "cases": out}) + "\n")
+    print("mdp kat", len(out), "cases;", sum(len(e.get("steps", [])) for r in out for e in r["episodes"]), "steps")
+
+
 def main():
     base, node_mod, pbn_mod = refload.load_hot_path()
     only = set(sys.argv[1:])
@@ -334,6 +496,10 @@ def main():
     if not only or "mt" in only:
         gen_r1_mt(base, "bittner28")
         gen_r1_mt(base, "bittner199", T=3000)
+    if not only or "logic" in only:
+        gen_logic()
+    if not only or "mdp" in only:
+        gen_mdp(node_mod, pbn_mod)
     multi = refload.load_multi_env()
     if not only or "r6" in only:
         gen_r6(base, multi, "bittner28", n_fixed=16, horizon=7, seeds=(1, 2, 3), n_steps=40, list_every=5)

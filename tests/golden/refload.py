@@ -12,6 +12,9 @@ none of which is installed; for that module only, inert import stand-ins are
 registered (an empty ``gymnasium.Env`` base class, space classes that just
 record their arguments, a pass-through ``njit``, dict subclasses for the
 colomoto types). None of them is on the computed path of ``step()``.
+The macro-action env modules (``pbn_env.py``, ``pbcn_env.py``, ``sampled_data.py``,
+``self_triggering.py``) use the same stand-ins; their spaces' ``contains`` accepts
+everything (only valid actions are fed), so action validation is not pinned.
 """
 
 from __future__ import annotations
@@ -79,10 +82,18 @@ def _install_env_import_standins():
         spaces = types.ModuleType("gymnasium.spaces")
 
         class _Space:
+            """Records its arguments; ``n`` is the first one. ``contains`` accepts everything:
+            fixtures only ever feed valid actions, so action validation is not pinned by them."""
+
             def __init__(self, *a, **k):
                 self.args = a
+                self.n = a[0] if a else None
+                self.start = k.get("start", 0)
 
-        for n in ("Discrete", "MultiBinary", "MultiDiscrete", "Box"):
+            def contains(self, x):
+                return True
+
+        for n in ("Discrete", "MultiBinary", "MultiDiscrete", "Box", "Tuple"):
             setattr(spaces, n, type(n, (_Space,), {}))
         gym.spaces = spaces
         sys.modules["gymnasium"] = gym
@@ -117,6 +128,20 @@ def load_multi_env():
     _load("gym_PBN.utils.get_attractors_from_cabean", PKG / "utils" / "get_attractors_from_cabean.py")
     return _load("gym_PBN.envs.pbn_target_multi", PKG / "envs" / "pbn_target_multi.py",
                  package="gym_PBN.envs")
+
+
+def load_mdp_envs():
+    """Return the reference modules (pbn_env, pbcn_env, sampled_data, self_triggering, pbcn)."""
+    load_hot_path()
+    _install_env_import_standins()
+    common = PKG / "envs" / "common"
+    pbcn = _load("gym_PBN.envs.common.pbcn", common / "pbcn.py")
+    envs = PKG / "envs"
+    pbn_env = _load("gym_PBN.envs.pbn_env", envs / "pbn_env.py", package="gym_PBN.envs")
+    pbcn_env = _load("gym_PBN.envs.pbcn_env", envs / "pbcn_env.py", package="gym_PBN.envs")
+    sampled = _load("gym_PBN.envs.sampled_data", envs / "sampled_data.py", package="gym_PBN.envs")
+    selftrig = _load("gym_PBN.envs.self_triggering", envs / "self_triggering.py", package="gym_PBN.envs")
+    return pbn_env, pbcn_env, sampled, selftrig, pbcn
 
 
 def build_graph(base, predictor_sets, node_ids):

@@ -259,31 +259,3 @@ def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
     assert np.array_equal(got[idx], o.run_mt(seeds[idx], T))
     with pytest.raises(ValueError):
         G.PBNBatch("tt8", 2).mt_seed(np.array([1, 2**33], dtype=np.uint64))
-
-
-# ----------------------------------------------------------------- macro-action MDP wrappers (R4-based)
-def test_mdp_wrappers_step_conventions(G):
-    from gym_pbn_amd import mdp
-    from gym_pbn_amd.network import synthetic_truth_table_pbn
-
-    data = synthetic_truth_table_pbn(8, 3, 1)
-    data = [(m, t, n, i == 7) for i, (m, t, n, _) in enumerate(data)]  # node 7 as a control node
-    attractors = [{(0, 1, 0, 1, 0, 1, 0, 1)}, {(0, 0, 0, 0, 0, 0, 0, 0)}]
-    target = {(0, 0, 0, 0, 0, 0, 0, 0)}
-    e = mdp.PBNSampledDataEnv(data, attractors, target, T=6)
-    e.reset(options={"state": (0, 1, 1, 0, 1, 0, 1, 1)})
-    obs, r, term, trunc, info = e.step((3, 4))
-    assert info["interval"] == 3 and r <= 80 and obs.shape == (8,)
-    st = mdp.PBNSelfTriggeringEnv(data, attractors, target, T=5, rng_seed=0)
-    st.reset()
-    obs, r, term, trunc, info = st.step((0, 10))  # prob 1.0: exactly one step
-    assert info["interval"] == 1
-    c = mdp.PBCNSampledDataEnv(data, attractors, target, T=4)
-    assert c.M == 1 and c._idx_to_macro_action(3) == ([True], 2)  # i % 2^M -> control, i // 2^M + 1 -> interval
-    c.reset()
-    obs, r, term, trunc, info = c.step(2)
-    assert info["interval"] == 2 and info["control_action"] == [False]
-    cs = mdp.PBCNSelfTriggeringEnv(data, attractors, target, T=3, rng_seed=1)
-    cs.reset()
-    obs, r, term, trunc, info = cs.step(([True], 0.1))
-    assert 1 <= info["interval"] <= 3
