@@ -77,3 +77,43 @@ def test_shard_ranges():
     shards = [shard_for(r, 8, 1 << 20) for r in range(8)]
     assert [s.env_base for s in shards] == [r << 20 for r in range(8)]
     assert shards[0].n_global == 8 << 20
+
+
+def _gather_worker(rank, world, port, out_dir):
+    sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from gym_pbn_amd.rollout import alloc_chunk, gather_chunk
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    T, B, W = 3, 5, 4
+    c = alloc_chunk(T, B, W, "cpu")
+    g = torch.Generator().manual_seed(rank)
+    c["obs"].copy_(torch.randint(-2**62, 2**62, (T, B, W), generator=g))
+    c["reward"].copy_(torch.arange(T * B, dtype=torch.int32).view(T, B) + 1000 * rank)
+    c["flags"].copy_(torch.randint(0, 8, (T, B), generator=g).to(torch.uint8))
+    c["n_updates"].copy_(torch.randint(0, 5000, (T, B), generator=g).to(torch.int32))
+    out, works = gather_chunk(c, dist, async_op=True)
+    for w in works:
+        w.wait()
+    torch.save({k: v.clone() for k, v in c.items()}, Path(out_dir) / f"local{rank}.pt")
+    if rank == 0:
+        torch.save(out, Path(out_dir) / "gathered.pt")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trajectory_chunk_gather_is_rank_major(tmp_path):
+    """rollout.gather_chunk: [T][B_local]... per rank -> [world][T][B_local]..., every field (config 5)."""
+    import torch
+
+    world = 2
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = torch.load(tmp_path / "gathered.pt", weights_only=True)
+    for r in range(world):
+        loc = torch.load(tmp_path / f"local{r}.pt", weights_only=True)
+        for k, v in loc.items():
+            assert got[k].dtype == v.dtype and torch.equal(got[k][r], v), k

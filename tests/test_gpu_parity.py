@@ -259,3 +259,35 @@ def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
     assert np.array_equal(got[idx], o.run_mt(seeds[idx], T))
     with pytest.raises(ValueError):
         G.PBNBatch("tt8", 2).mt_seed(np.array([1, 2**33], dtype=np.uint64))
+
+
+# ----------------------------------------------------------------- config 5: device trajectory chunks
+def test_trajectory_collector_matches_host_api(G):
+    """rollout.TrajectoryCollector writes step t of a chunk into slice t; same results as the host API."""
+    import torch
+
+    from gym_pbn_amd.rollout import TrajectoryCollector
+
+    z = golden("r6_bittner28.npz")
+    net = G.Net(load_network("bittner28"))
+    cfg = G.EnvConfig(net, cubes_to_attractors(z, 28), horizon=6)
+    B, T, A = 3000, 6, 3
+    rng = np.random.default_rng(5)
+    acts = rng.integers(0, 29, size=(T, B, A)).astype(np.int32)
+    acts[rng.random(acts.shape) < 0.6] = 0
+    dev = torch.device("cuda", 0)
+    b1 = G.PBNBatch(net, B, seed=77, env_id_base=123)
+    col = TrajectoryCollector(b1, cfg, T, A, dev, update_cap=1 << 16)
+    buf, gathered = col.step_chunk(torch.from_numpy(acts).to(dev))
+    col.finish()
+    assert gathered is None
+    b2 = G.PBNBatch(net, B, seed=77, env_id_base=123)
+    b2.env_reset(cfg)
+    for t in range(T):
+        obs, rew, flags, nup = b2.env_step_multi(cfg, acts[t], update_cap=1 << 16)
+        assert np.array_equal(buf["obs"][t].cpu().numpy().view(np.uint64), obs), t
+        assert np.array_equal(buf["reward"][t].cpu().numpy(), rew), t
+        assert np.array_equal(buf["flags"][t].cpu().numpy(), flags), t
+        assert np.array_equal(buf["n_updates"][t].cpu().numpy().view(np.uint32), nup), t
+    assert (flags & 2).all()  # truncated at the horizon == T
+    assert np.array_equal(b1.get_state(), b2.get_state())
