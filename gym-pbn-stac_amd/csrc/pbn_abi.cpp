@@ -91,7 +91,8 @@ struct pbn_envcfg {
     int W = 0, H = 0, H_reset = 0;
     std::vector<uint8_t> image;  // net image + cubes [H][2][W] + target [2][W]
     NetLayout L{};
-    uint32_t off_cubes = 0, off_target = 0, off_nodemask = 0;
+    uint32_t off_cubes = 0, off_target = 0, off_ndelta = 0;
+    int fast = 0;
     std::vector<uint64_t> reset_care, reset_value;
     int32_t horizon = 100, reward_success = 1000, action_cost = 1;
     std::mutex mu;
@@ -211,26 +212,34 @@ static int build_predictor_image(const pbn_net_desc* d, pbn_net* n) {
     for (int j = 0; j < 3 * P; j++)
         if (d->pred_inputs[j] < 0 || d->pred_inputs[j] >= N)
             return fail(PBN_E_RANGE, "predictor input %d out of range [0, %d)", d->pred_inputs[j], N);
+    uint32_t pmax = 1;
+    for (int i = 0; i < N; i++) pmax = std::max(pmax, (uint32_t)(d->pred_offsets[i + 1] - d->pred_offsets[i]));
     NetLayout L{};
+    L.tp = (pmax - 1 + 1) & ~1u;
+    L.pmax = pmax;
     L.off_node = 0;
-    L.off_thr = align16(4u * (uint32_t)N);
-    L.off_rec = align16(L.off_thr + 8u * (uint32_t)P);
-    L.bytes = align16(L.off_rec + 8u * (uint32_t)P);
+    L.off_thr = 0;
+    L.off_rec = align16(8u * L.tp * (uint32_t)N);
+    L.bytes = align16(L.off_rec + 8u * pmax * (uint32_t)N);
     L.kind = KIND_PREDICTOR_MIX;
     L.n_nodes = N;
     if (L.bytes > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "network tables (%u B) exceed the LDS budget", L.bytes);
     n->image.assign(L.bytes, 0);
     uint8_t* im = n->image.data();
     for (int i = 0; i < N; i++) {
-        uint32_t o0 = (uint32_t)d->pred_offsets[i], c = (uint32_t)(d->pred_offsets[i + 1] - d->pred_offsets[i]);
-        uint32_t v = o0 | (c << 16);
-        memcpy(im + L.off_node + 4 * i, &v, 4);
-    }
-    for (int j = 0; j < P; j++) {
-        memcpy(im + L.off_thr + 8 * j, &d->pred_thr[j], 8);
-        uint64_t rec = (uint64_t)(uint32_t)d->pred_inputs[3 * j] | ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 1] << 16) |
-                       ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 2] << 32) | ((uint64_t)d->pred_tt[j] << 48);
-        memcpy(im + L.off_rec + 8 * j, &rec, 8);
+        const int o0 = d->pred_offsets[i], c = d->pred_offsets[i + 1] - d->pred_offsets[i];
+        for (uint32_t q = 0; q < L.tp; q++) {
+            // predictor j is skipped iff k53 >= thr[j]; thresholds past the last-but-one never are
+            const uint64_t t = (int)q < c - 1 ? d->pred_thr[o0 + q] : ~0ull;
+            memcpy(im + L.off_thr + 8 * ((size_t)i * L.tp + q), &t, 8);
+        }
+        for (int q = 0; q < c; q++) {
+            const int j = o0 + q;
+            uint64_t rec = (uint64_t)(uint32_t)d->pred_inputs[3 * j] |
+                           ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 1] << 16) |
+                           ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 2] << 32) | ((uint64_t)d->pred_tt[j] << 48);
+            memcpy(im + L.off_rec + 8 * ((size_t)i * pmax + q), &rec, 8);
+        }
     }
     n->L = L;
     return 0;
@@ -776,8 +785,8 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
     c->L = net->L;
     c->off_cubes = net->L.bytes;
     c->off_target = align16(c->off_cubes + 16u * (uint32_t)W * (uint32_t)c->H);
-    c->off_nodemask = align16(c->off_target + 16u * (uint32_t)W);
-    uint32_t bytes = align16(c->off_nodemask + 8u * (uint32_t)net->N);
+    c->off_ndelta = align16(c->off_target + 16u * (uint32_t)W);
+    uint32_t bytes = align16(c->off_ndelta + 8u * (uint32_t)net->N);
     if (bytes > MAX_IMAGE) {
         delete c;
         return fail(PBN_E_UNSUPPORTED, "network + %d attractor cubes exceed the LDS budget", d->n_cubes);
@@ -796,17 +805,32 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
         tgt[k] = d->target_care[k];
         tgt[W + k] = d->target_value[k] & d->target_care[k];
     }
-    // per node i: bit h of .x = cube h cares about i, bit h of .y = its value (first 32 cubes)
-    uint32_t* nm = reinterpret_cast<uint32_t*>(c->image.data() + c->off_nodemask);
+    // Fast attractor test: one byte counter per cube (<= 8 cubes) holding the number of cared
+    // bits where the state differs from the cube. Node i going 0 -> 1 adds +1 to the cubes
+    // that want it 0 and -1 to those that want it 1; per node that is one packed delta
+    // d = plus - minus per 32-bit half (bytes 0-3 = cubes 0-3, 4-7 = cubes 4-7). The
+    // counters never leave [0, 255], so M += d (or M -= d for 1 -> 0) is exact word arithmetic.
+    int max_care = 0;
+    for (int h = 0; h < c->H; h++) {
+        int pc = 0;
+        for (int k = 0; k < W; k++) pc += __builtin_popcountll(d->cube_care[(size_t)h * W + k]);
+        max_care = std::max(max_care, pc);
+    }
+    c->fast = (c->H <= 8 && max_care <= 255) ? 1 : 0;
+    uint32_t* nd = reinterpret_cast<uint32_t*>(c->image.data() + c->off_ndelta);
     for (int i = 0; i < net->N; i++) {
-        uint32_t care = 0, val = 0;
-        for (int h = 0; h < c->H && h < 32; h++) {
+        uint32_t plus[2] = {0, 0}, minus[2] = {0, 0};
+        for (int h = 0; h < c->H && h < 8; h++) {
             const uint64_t cw = d->cube_care[(size_t)h * W + i / 64], vw = d->cube_value[(size_t)h * W + i / 64];
-            care |= (uint32_t)((cw >> (i % 64)) & 1u) << h;
-            val |= (uint32_t)((cw & vw) >> (i % 64) & 1u) << h;
+            if (!((cw >> (i % 64)) & 1u)) continue;
+            const uint32_t byte = 1u << (8 * (h & 3));
+            if ((vw >> (i % 64)) & 1u)
+                minus[h >> 2] |= byte;
+            else
+                plus[h >> 2] |= byte;
         }
-        nm[2 * i] = care;
-        nm[2 * i + 1] = val;
+        nd[2 * i] = plus[0] - minus[0];
+        nd[2 * i + 1] = plus[1] - minus[1];
     }
     c->L.bytes = bytes;
     c->reset_care.assign(d->reset_care, d->reset_care + (size_t)c->H_reset * W);
@@ -873,7 +897,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     const pbn_envcfg::Dev* dv = cfg->on(b->device);
     if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
     int bpc = 1;
-    if (int e = max_blocks_env(b->W, b->net->kind, cfg->L.bytes, &bpc))
+    if (int e = max_blocks_env(b->W, b->net->kind, cfg->fast, cfg->L.bytes, &bpc))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
     EnvArgs a{};
     a.state = b->d_state;
@@ -888,7 +912,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.L = cfg->L;
     a.off_cubes = cfg->off_cubes;
     a.off_target = cfg->off_target;
-    a.off_nodemask = cfg->off_nodemask;
+    a.off_ndelta = cfg->off_ndelta;
+    a.fast = cfg->fast;
     if (int rc = b->s_counter.ensure(8)) return rc;
     a.counter = (unsigned long long*)b->s_counter.p;
     a.n_cubes = cfg->H;

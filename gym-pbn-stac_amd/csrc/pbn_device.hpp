@@ -129,51 +129,6 @@ __device__ __forceinline__ void stage_image(const uint4* __restrict__ img, uint3
 }
 
 // ---------------------------------------------------------------- node updates
-// Bittner Predstep (base.py:89-119) in integer form.
-//   node_info[i] = first predictor (low 16) | predictor count (high 16)
-//   thr[j]      = 53-bit selection threshold, rec[j] = in0 | in1<<16 | in2<<32 | tt<<48
-template <int W>
-__device__ __forceinline__ uint32_t predictor_update(uint64_t (&s)[W], uint32_t i, uint64_t k53, const uint8_t* lds,
-                                                     const NetLayout& L) {
-    const uint32_t info = reinterpret_cast<const uint32_t*>(lds + L.off_node)[i];
-    const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
-    const uint64_t* thr = reinterpret_cast<const uint64_t*>(lds + L.off_thr);
-    uint32_t j = o0;
-    for (uint32_t q = 1; q < cnt; ++q) j += (k53 >= thr[o0 + q - 1]) ? 1u : 0u;
-    const uint64_t rec = reinterpret_cast<const uint64_t*>(lds + L.off_rec)[j];
-    const uint32_t p = (getbit<W>(s, (uint32_t)rec & 0xFFFFu) << 3) |
-                       (getbit<W>(s, (uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
-                       (getbit<W>(s, (uint32_t)(rec >> 32) & 0xFFFFu) << 1) | getbit<W>(s, i);
-    const uint32_t y = (uint32_t)(rec >> (48 + p)) & 1u;
-    setbit<W>(s, i, y);
-    return y;
-}
-
-// PBN node update (common/node.py:31-38): k53 < ceil(p * 2^53), table index in C order.
-//   node_info[i] = thr offset (low 32) | input offset (bits 32..47) | k (bits 48..55)
-template <int W>
-__device__ __forceinline__ uint32_t table_update(uint64_t (&s)[W], uint32_t i, uint64_t k53, const uint8_t* lds,
-                                                 const NetLayout& L) {
-    const uint64_t info = reinterpret_cast<const uint64_t*>(lds + L.off_node)[i];
-    const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu, k = (uint32_t)(info >> 48) & 0xFFu;
-    const uint16_t* in = reinterpret_cast<const uint16_t*>(lds + L.off_rec) + ioff;
-    uint32_t idx = 0;
-    for (uint32_t q = 0; q < k; ++q) idx = (idx << 1) | getbit<W>(s, in[q]);
-    const uint64_t t = reinterpret_cast<const uint64_t*>(lds + L.off_thr)[toff + idx];
-    const uint32_t y = k53 < t ? 1u : 0u;
-    setbit<W>(s, i, y);
-    return y;
-}
-
-template <int W, int KIND>
-__device__ __forceinline__ uint32_t node_update(uint64_t (&s)[W], uint32_t i, uint64_t k53, const uint8_t* lds,
-                                                const NetLayout& L) {
-    if constexpr (KIND == KIND_PREDICTOR_MIX)
-        return predictor_update<W>(s, i, k53, lds, L);
-    else
-        return table_update<W>(s, i, k53, lds, L);
-}
-
 // Philox (node, k53) for update counter c0/c1 of env gid.
 //   Bittner: node in [0, N-1] (base.py:308); PBN: node in [1, N-1] (pbn.py:131).
 template <int KIND>
@@ -196,17 +151,21 @@ struct PlaneT {
 using Plane = PlaneT<BLOCK>;
 
 // Bittner Predstep (base.py:89-119) evaluated on the LDS plane: the new value of node i.
-// `self` is the dword holding node i (already read by the caller).
+// `self` is the dword holding node i (already read by the caller). Predictor choice
+// (base.py:94-97): j = #{q : k53 >= thr[i][q]} over the padded thresholds (the padding
+// never counts, so j <= count - 1: Python's for/break falling through to the last one).
+// Thresholds and record are both addressed by i alone, and the threshold loop has a
+// wave-uniform trip count (L.tp), so lanes do not diverge on per-node predictor counts.
 template <class P_t>
 __device__ __forceinline__ uint32_t predictor_eval_lds(const P_t& P, uint32_t i, uint32_t self, uint64_t k53,
                                                        const uint8_t* tbl, const NetLayout& L) {
-    const uint32_t info = reinterpret_cast<const uint32_t*>(tbl + L.off_node)[i];
-    const uint32_t o0 = info & 0xFFFFu, cnt = info >> 16;
-    const uint64_t* thr = reinterpret_cast<const uint64_t*>(tbl + L.off_thr) + o0;
+    const ulonglong2* thr = reinterpret_cast<const ulonglong2*>(tbl + L.off_thr) + (i * L.tp >> 1);
     uint32_t j = 0;
-#pragma unroll 4
-    for (uint32_t q = 0; q + 1 < cnt; ++q) j += (k53 >= thr[q]) ? 1u : 0u;
-    const uint64_t rec = reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[o0 + j];
+    for (uint32_t q = 0; q < (L.tp >> 1); ++q) {
+        const ulonglong2 t = thr[q];
+        j += (k53 >= t.x ? 1u : 0u) + (k53 >= t.y ? 1u : 0u);
+    }
+    const uint64_t rec = reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[i * L.pmax + j];
     const uint32_t p = (P.bit((uint32_t)rec & 0xFFFFu) << 3) | (P.bit((uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
                        (P.bit((uint32_t)(rec >> 32) & 0xFFFFu) << 1) | ((self >> (i & 31u)) & 1u);
     return (uint32_t)(rec >> (48 + p)) & 1u;

@@ -206,15 +206,17 @@ __device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* c
 // heavy-tailed until-attractor loops (1 .. 10^4 updates) do not idle the other
 // 63 lanes of the wave. The env's state lives in the lane's LDS plane column.
 //
-// Attractor test (is_attracting_state :489-492 == "matches some cube"): for
-// H <= ENV_HMAX cubes each lane keeps, per cube, the number of cared bits that
-// differ; an update that flips node i adjusts the counters of the cubes caring
-// about i (per-node cube masks in LDS), so the test is O(H) register work per
-// update. Larger cube sets fall back to a full match after every change.
-constexpr int ENV_HMAX = 8;
+// Attractor test (is_attracting_state :489-492 == "matches some cube").
+// FAST (<= 8 cubes, each caring about <= 255 nodes): the lane keeps one byte per
+// cube counting the cared bits where the state differs from the cube, packed in
+// two words; an update that flips node i adds the node's packed delta (or its
+// negation), and "some cube matches" is a zero-byte test -- a handful of VALU ops
+// per update. Otherwise the state is matched against every cube after a change.
 constexpr int ENV_CHUNK = 16;  // updates between refill rounds
 
-template <int W, int KIND, int REPLAY>
+__device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
+
+template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
@@ -223,15 +225,15 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     const uint32_t N = (uint32_t)a.L.n_nodes;
     const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
     const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
-    const uint2* nmask = reinterpret_cast<const uint2*>(lds + a.off_nodemask);
+    const uint2* ndelta = reinterpret_cast<const uint2*>(lds + a.off_ndelta);
     const int32_t H = a.n_cubes;
-    const bool fast = H <= ENV_HMAX;
     const uint32_t lane = __lane_id();
 
     int64_t e = -1;
     bool exhausted = false;
     uint64_t o0[W];
-    uint32_t M[ENV_HMAX];
+    uint32_t m_lo = 0, m_hi = 0;  // FAST: packed per-cube mismatch counters
+    bool hit0 = false;            // o0 is attracting (the test made after the first update)
     uint32_t used = 0;
     int64_t nst = 0, dpos = 0, dend = 0;
     int n_act = 0;
@@ -264,9 +266,19 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
                         for (int k = 0; k < W; ++k) o0[k] = s[k];  // :133 observation before the update
                         to_plane<W>(P, s);
-#pragma unroll
-                        for (int h = 0; h < ENV_HMAX; ++h)
-                            M[h] = (fast && h < H) ? cube_mismatch<W>(s, cubes + (uint64_t)h * 2 * W) : 1u;
+                        if constexpr (FAST) {
+                            uint32_t m[2] = {0x01010101u, 0x01010101u};  // unused cubes: never zero
+                            for (int32_t h = 0; h < H; ++h) {
+                                const uint32_t c = cube_mismatch<W>(s, cubes + (uint64_t)h * 2 * W);
+                                const uint32_t sh = 8u * (uint32_t)(h & 3);
+                                m[h >> 2] = (m[h >> 2] & ~(0xFFu << sh)) | (c << sh);
+                            }
+                            m_lo = m[0];
+                            m_hi = m[1];
+                            hit0 = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
+                        } else {
+                            hit0 = attracting<W>(o0, cubes, H);
+                        }
                         used = 0;
                         capped = false;
                         if constexpr (REPLAY) {
@@ -316,35 +328,17 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 changed = table_update_lds(P, i, k53, lds, a.L);
             ++used;
             bool hit;
-            if (fast) {
+            if constexpr (FAST) {
+                const uint2 d = ndelta[i];
+                const uint32_t y = P.bit(i);
+                const uint32_t dl = changed ? (y ? d.x : 0u - d.x) : 0u;
+                const uint32_t dh = changed ? (y ? d.y : 0u - d.y) : 0u;
+                m_lo += dl;
+                m_hi += dh;
                 // :134 the first update is never tested: the check at used == 1 is on o0
-                bool any0 = false;
-#pragma unroll
-                for (int h = 0; h < ENV_HMAX; ++h) any0 |= (h < H) && (M[h] == 0u);
-                if (used == 1 && any0) {
-                    hit = true;
-                } else {
-                    if (changed) {
-                        const uint2 m = nmask[i];
-                        const uint32_t y = P.bit(i);
-#pragma unroll
-                        for (int h = 0; h < ENV_HMAX; ++h) {
-                            const uint32_t care = (m.x >> h) & 1u, v = (m.y >> h) & 1u;
-                            M[h] = M[h] + (care ? ((y != v) ? 1u : 0xFFFFFFFFu) : 0u);
-                        }
-                    }
-                    if (used == 1) {
-                        hit = false;
-                    } else {
-                        bool z = false;
-#pragma unroll
-                        for (int h = 0; h < ENV_HMAX; ++h) z |= (h < H) && (M[h] == 0u);
-                        hit = z;
-                    }
-                }
+                hit = used == 1 ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
             } else {
-                hit = (used == 1) ? attracting<W>(o0, cubes, H)
-                                  : ((changed || used == 2) && attracting_plane<W>(P, cubes, H));
+                hit = (used == 1) ? hit0 : ((changed || used == 2) && attracting_plane<W>(P, cubes, H));
             }
             if (hit) {
                 done = true;
@@ -398,9 +392,11 @@ static void* step_fn_w(int W, int store, int replay, int sb) {
 }
 
 template <int KIND>
-static void* env_fn_w(int W, int replay) {
-#define PBN_ENV_CASE(w) \
-    case w: return replay ? (void*)k_env<w, KIND, 1> : (void*)k_env<w, KIND, 0>;
+static void* env_fn_w(int W, int replay, int fast) {
+#define PBN_ENV_CASE(w)                                                                  \
+    case w:                                                                              \
+        if (fast) return replay ? (void*)k_env<w, KIND, 1, 1> : (void*)k_env<w, KIND, 0, 1>; \
+        return replay ? (void*)k_env<w, KIND, 1, 0> : (void*)k_env<w, KIND, 0, 0>;
     switch (W) {
         PBN_ENV_CASE(1)
         PBN_ENV_CASE(2)
@@ -485,8 +481,8 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream) {
 }
 
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream) {
-    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay)
-                                              : env_fn_w<KIND_PROB_TABLE>(W, replay);
+    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast)
+                                              : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast);
     EnvArgs c = a;
     return launch(fn, grid, env_lds_bytes(W, a.L.bytes), stream, &c, sizeof c);
 }
@@ -510,8 +506,9 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
 
 uint32_t env_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK; }
 
-int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu) {
-    void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0) : env_fn_w<KIND_PROB_TABLE>(W, 0);
+int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu) {
+    void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast)
+                                          : env_fn_w<KIND_PROB_TABLE>(W, 0, fast);
     return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes), blocks_per_cu);
 }
 

@@ -22,13 +22,20 @@ constexpr int MAX_WORDS = 8;        // N <= 512
 constexpr uint32_t MAX_IMAGE = 48 * 1024;  // LDS bytes for the network image (+ 16 KiB state planes)
 
 // Byte offsets of the tables inside the LDS image (16-byte aligned image).
+// Predictor-mix networks use a padded per-node layout so that both table reads of an
+// update are addressed by the node index alone (no dependent "node info" read):
+//   thr [N][tp]   u64 selection thresholds, tp = max predictors - 1 rounded up to even,
+//                 padding = UINT64_MAX (never reached: k53 < 2^53)
+//   rec [N][pmax] u64 records in0 | in1<<16 | in2<<32 | tt<<48
 struct NetLayout {
-    uint32_t off_node;  // per-node info
+    uint32_t off_node;  // per-node info (truth-table networks)
     uint32_t off_thr;   // u64 thresholds
     uint32_t off_rec;   // predictor records (u64) or input lists (u16)
     uint32_t bytes;     // total, multiple of 16
     int32_t kind;
     int32_t n_nodes;
+    uint32_t tp;        // predictor mix: thresholds per node (even)
+    uint32_t pmax;      // predictor mix: record slots per node
 };
 
 struct StepArgs {
@@ -78,9 +85,10 @@ struct EnvArgs {
     NetLayout L;
     uint32_t off_cubes;      // care/value pairs [H][2][W] u64 inside the LDS image
     uint32_t off_target;     // target care/value [2][W]
-    uint32_t off_nodemask;   // per node: {cubes caring about it, their values} as u32 bit masks
+    uint32_t off_ndelta;     // per node: uint2 packed mismatch-counter deltas (fast attractor test)
     unsigned long long* counter;  // work-queue head (zeroed per launch)
     int32_t n_cubes;
+    int32_t fast;            // 1: <= 8 cubes, each caring about <= 255 nodes (byte counters)
     uint64_t B, env_base, seed;
     uint32_t call_idx, update_cap;
     int32_t A, offset, dedup, horizon, reward_success, action_cost;
@@ -138,7 +146,7 @@ int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
-int max_blocks_env(int W, int kind, uint32_t lds_bytes, int* blocks_per_cu);
+int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes);
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
