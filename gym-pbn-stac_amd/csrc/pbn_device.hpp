@@ -15,9 +15,12 @@ namespace pbn {
 // Random123's Philox4x32 with 10 rounds (KAT-checked in tests/test_oracle.py and
 // tests/test_gpu_parity.py). Each round is two 32x32->64 multiplies
 // (v_mad_u64_u32) and four XORs.
+#ifndef PBN_PHILOX_ROUNDS
+#define PBN_PHILOX_ROUNDS 10  // only measurement builds (tools/) change this
+#endif
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < PBN_PHILOX_ROUNDS; ++r) {
         if (r) {
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
@@ -156,19 +159,29 @@ using Plane = PlaneT<BLOCK>;
 // never counts, so j <= count - 1: Python's for/break falling through to the last one).
 // Thresholds and record are both addressed by i alone, and the threshold loop has a
 // wave-uniform trip count (L.tp), so lanes do not diverge on per-node predictor counts.
-template <class P_t>
-__device__ __forceinline__ uint32_t predictor_eval_lds(const P_t& P, uint32_t i, uint32_t self, uint64_t k53,
-                                                       const uint8_t* tbl, const NetLayout& L) {
+__device__ __forceinline__ uint64_t predictor_record(uint32_t i, uint64_t k53, const uint8_t* tbl,
+                                                     const NetLayout& L) {
     const ulonglong2* thr = reinterpret_cast<const ulonglong2*>(tbl + L.off_thr) + (i * L.tp >> 1);
     uint32_t j = 0;
     for (uint32_t q = 0; q < (L.tp >> 1); ++q) {
         const ulonglong2 t = thr[q];
         j += (k53 >= t.x ? 1u : 0u) + (k53 >= t.y ? 1u : 0u);
     }
-    const uint64_t rec = reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[i * L.pmax + j];
+    return reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[i * L.pmax + j];
+}
+
+// Y = rec.tt[x_in0 x_in1 x_in2 x_self] (base.py:100-118 via the exported truth table).
+template <class P_t>
+__device__ __forceinline__ uint32_t predictor_apply(const P_t& P, uint32_t i, uint32_t self, uint64_t rec) {
     const uint32_t p = (P.bit((uint32_t)rec & 0xFFFFu) << 3) | (P.bit((uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
                        (P.bit((uint32_t)(rec >> 32) & 0xFFFFu) << 1) | ((self >> (i & 31u)) & 1u);
     return (uint32_t)(rec >> (48 + p)) & 1u;
+}
+
+template <class P_t>
+__device__ __forceinline__ uint32_t predictor_eval_lds(const P_t& P, uint32_t i, uint32_t self, uint64_t k53,
+                                                       const uint8_t* tbl, const NetLayout& L) {
+    return predictor_apply(P, i, self, predictor_record(i, k53, tbl, L));
 }
 
 // PBN Node.compute_next_value (common/node.py:31-38) evaluated on the LDS plane.

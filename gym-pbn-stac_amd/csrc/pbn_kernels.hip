@@ -35,17 +35,95 @@ namespace pbn {
 // SB (threads per workgroup) trades LDS staging traffic against scheduling
 // granularity: the image is staged once per workgroup, so 1024-thread groups
 // read it from L2 4x less often than 256-thread groups.
+// One update per env (T == 1), Philox. Envs are taken in pairs (e, e + stride); at the
+// bench sizes every thread owns exactly one pair. The pair's draws and (for predictor
+// networks) its predictor records depend only on (seed, update counter, env id), so
+// they are computed while the pair's state loads are in flight.
+template <int W, int KIND, int STORE, int SB>
+__device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, uint64_t e, uint64_t stride,
+                                              uint64_t (&cur)[W], uint32_t N) {
+    const uint64_t u = a.update_base;
+    uint64_t nxt[W];
+    uint32_t i0 = 0, i1 = 0;
+    uint64_t q0 = 0, q1 = 0;
+    auto draws = [&](uint64_t ea) {
+        uint32_t w0[4], w1[4];
+        philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), a.env_base + ea, STREAM_STEP, w0);
+        philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), a.env_base + ea + stride, STREAM_STEP, w1);
+        i0 = philox_node<KIND>(w0[0], N);
+        i1 = philox_node<KIND>(w1[0], N);
+        q0 = k53_of(w0[1], w0[2]);
+        q1 = k53_of(w1[1], w1[2]);
+    };
+    if (e + stride < a.B) load_state<W>(a.state + (e + stride) * W, nxt);
+    draws(e);
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    __syncthreads();
+    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+    while (e < a.B) {
+        const uint64_t e1 = e + stride;
+        uint64_t r0 = 0, r1 = 0;
+        if constexpr (KIND == KIND_PREDICTOR_MIX) {  // state-independent: before the loads land
+            r0 = predictor_record(i0, q0, lds, a.L);
+            r1 = predictor_record(i1, q1, lds, a.L);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t eh = h ? e1 : e;
+            if (eh >= a.B) break;
+            uint64_t(&s)[W] = h ? nxt : cur;
+            to_plane<W>(P, s);
+            const uint32_t i = h ? i1 : i0;
+            const uint32_t d = i >> 5, sh = i & 31u;
+            const uint32_t self = P.get(d);
+            uint32_t y;
+            if constexpr (KIND == KIND_PREDICTOR_MIX)
+                y = predictor_apply(P, i, self, h ? r1 : r0);
+            else
+                y = table_eval_lds(P, i, h ? q1 : q0, lds, a.L);
+            const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+            if constexpr (STORE == STORE_DIRTY) {
+                if (nv != self) {  // only the 16-B half holding node i can have changed
+                    P.put(d, nv);
+                    uint64_t out[W];
+                    from_plane<W>(P, out);
+                    store_dirty<W>(a.state + eh * W, out, 1u << (i >> 6));
+                }
+            } else {
+                P.put(d, nv);
+                uint64_t out[W];
+                from_plane<W>(P, out);
+                store_state<W>(a.state + eh * W, out);
+            }
+        }
+        e = e1 + stride;
+        if (e < a.B) {
+            load_state<W>(a.state + e * W, cur);
+            if (e + stride < a.B) load_state<W>(a.state + (e + stride) * W, nxt);
+            draws(e);
+        }
+    }
+}
+
 template <int W, int KIND, int STORE, int REPLAY, int SB>
 __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     const uint64_t stride = (uint64_t)gridDim.x * SB;
     uint64_t e = (uint64_t)blockIdx.x * SB + threadIdx.x;
+    const uint32_t N = (uint32_t)a.L.n_nodes;
     uint64_t cur[W];
     if (e < a.B) load_state<W>(a.state + e * W, cur);
+    if constexpr (!REPLAY) {
+        if (a.T == 1) {
+            // Step mode: the draws depend on (seed, update counter, env id) only, so every
+            // draw this thread needs is computed while its state loads are in flight.
+            k_step_single<W, KIND, STORE, SB>(a, lds, e, stride, cur, N);
+            return;
+        }
+    }
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
-    const uint32_t N = (uint32_t)a.L.n_nodes;
     while (e < a.B) {
         const uint64_t en = e + stride;
         uint64_t nxt[W];
