@@ -896,9 +896,15 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
                       const void* d_off, const void* d_di, const void* d_dk) {
     const pbn_envcfg::Dev* dv = cfg->on(b->device);
     if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
+    // cooperative draw generation: predictor mix, Philox, record index fits the u16 entry
+    const int mode = (cfg->fast && !replay && b->net->kind == KIND_PREDICTOR_MIX && cfg->L.pmax <= 16 &&
+                      b->net->N <= 512 && !getenv("PBNSIM_ENV_NO_GEN"))
+                         ? 2
+                         : cfg->fast;
     int bpc = 1;
-    if (int e = max_blocks_env(b->W, b->net->kind, cfg->fast, cfg->L.bytes, &bpc))
+    if (int e = max_blocks_env(b->W, b->net->kind, mode, cfg->L.bytes, &bpc))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
+    if (const char* v = getenv("PBNSIM_ENV_BPC")) bpc = std::max(1, std::min(bpc, atoi(v)));  // tuning knob
     EnvArgs a{};
     a.state = b->d_state;
     a.n_steps = b->d_nsteps;
@@ -913,7 +919,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.off_cubes = cfg->off_cubes;
     a.off_target = cfg->off_target;
     a.off_ndelta = cfg->off_ndelta;
-    a.fast = cfg->fast;
+    a.fast = mode;
+    a.off_gen = cfg->L.bytes + 8u * (uint32_t)b->W * BLOCK;
     if (int rc = b->s_counter.ensure(8)) return rc;
     a.counter = (unsigned long long*)b->s_counter.p;
     a.n_cubes = cfg->H;

@@ -159,7 +159,7 @@ using Plane = PlaneT<BLOCK>;
 // never counts, so j <= count - 1: Python's for/break falling through to the last one).
 // Thresholds and record are both addressed by i alone, and the threshold loop has a
 // wave-uniform trip count (L.tp), so lanes do not diverge on per-node predictor counts.
-__device__ __forceinline__ uint64_t predictor_record(uint32_t i, uint64_t k53, const uint8_t* tbl,
+__device__ __forceinline__ uint32_t predictor_choice(uint32_t i, uint64_t k53, const uint8_t* tbl,
                                                      const NetLayout& L) {
     const ulonglong2* thr = reinterpret_cast<const ulonglong2*>(tbl + L.off_thr) + (i * L.tp >> 1);
     uint32_t j = 0;
@@ -167,7 +167,12 @@ __device__ __forceinline__ uint64_t predictor_record(uint32_t i, uint64_t k53, c
         const ulonglong2 t = thr[q];
         j += (k53 >= t.x ? 1u : 0u) + (k53 >= t.y ? 1u : 0u);
     }
-    return reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[i * L.pmax + j];
+    return j;
+}
+
+__device__ __forceinline__ uint64_t predictor_record(uint32_t i, uint64_t k53, const uint8_t* tbl,
+                                                     const NetLayout& L) {
+    return reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[i * L.pmax + predictor_choice(i, k53, tbl, L)];
 }
 
 // Y = rec.tt[x_in0 x_in1 x_in2 x_self] (base.py:100-118 via the exported truth table).

@@ -15,6 +15,8 @@
 //   k_env     PBNTargetMultiEnv.step pbn_target_multi.py:119-154
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pbn_device.hpp"
 #include "pbn_params.hpp"
 
@@ -290,12 +292,20 @@ __device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* c
 // two words; an update that flips node i adds the node's packed delta (or its
 // negation), and "some cube matches" is a zero-byte test -- a handful of VALU ops
 // per update. Otherwise the state is matched against every cube after a change.
-constexpr int ENV_CHUNK = 16;  // updates between refill rounds
+//
+// GEN (FAST == 2, predictor-mix networks, Philox): before each chunk the whole wave
+// generates the chunk's draws for all its active lanes -- assignment k of
+// n_active * ENV_CHUNK goes to lane k % 64 -- and stores (node, chosen predictor) as
+// u16 in a per-wave LDS buffer; the lanes then only apply the records. With every lane
+// active this is the same Philox work per lane; in the tail, when a few lanes run long
+// (capped) loops, idle lanes generate their draws and the per-update cost drops to the
+// state read/write.
 
 __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
+    static_assert(FAST != 2 || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
     extern __shared__ __align__(16) uint8_t lds[];
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
@@ -344,7 +354,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
                         for (int k = 0; k < W; ++k) o0[k] = s[k];  // :133 observation before the update
                         to_plane<W>(P, s);
-                        if constexpr (FAST) {
+                        if constexpr (FAST >= 1) {
                             uint32_t m[2] = {0x01010101u, 0x01010101u};  // unused cubes: never zero
                             for (int32_t h = 0; h < H; ++h) {
                                 const uint32_t c = cube_mismatch<W>(s, cubes + (uint64_t)h * 2 * W);
@@ -367,16 +377,82 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 }
             }
         }
-        if (__ballot(e >= 0) == 0) {
+        const uint64_t act = __ballot(e >= 0);
+        if (act == 0) {
             if (__ballot(!exhausted) == 0) break;
             continue;
+        }
+        uint16_t* gbuf = nullptr;
+        if constexpr (FAST == 2) {
+            // ---- cooperative draw generation for the next ENV_CHUNK updates of every active lane
+            uint8_t* gw = lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES;
+            gbuf = reinterpret_cast<uint16_t*>(gw);                                   // [ENV_CHUNK][64]
+            uint8_t* lane_of_rank = gw + ENV_CHUNK * 128;                             // [64]
+            uint32_t* used_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64);  // [64]
+            uint64_t* gid_tab = reinterpret_cast<uint64_t*>(gw + ENV_CHUNK * 128 + 64 + 256);  // [64]
+            const uint32_t nact = (uint32_t)__popcll(act);
+            if (e >= 0) {
+                lane_of_rank[__popcll(act & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+                used_tab[lane] = used;
+                gid_tab[lane] = a.env_base + (uint64_t)e;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t total = nact * ENV_CHUNK;
+            // k / nact as a multiply-high by ceil(2^32 / nact): exact for k < 2^16 (nact == 1 handled apart,
+            // its multiplier 2^32 does not fit 32 bits)
+            const uint32_t magic = nact > 1 ? (uint32_t)((0x100000000ull + nact - 1) / nact) : 0u;
+            for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                if (k < total) {
+                    const uint32_t sl = nact > 1 ? __umulhi(k, magic) : k, r = k - sl * nact;
+                    const uint32_t t = lane_of_rank[r];
+                    uint32_t w[4];
+                    philox_draw(a.seed, used_tab[t] + sl, a.call_idx, gid_tab[t], STREAM_ENV, w);
+                    const uint32_t i = philox_node<KIND>(w[0], N);
+                    const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
+                    gbuf[sl * 64 + t] = (uint16_t)(i | (j << 9));
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (e < 0) continue;
 
         // ---- up to ENV_CHUNK updates of this lane's env
         const uint64_t g = a.env_base + (uint64_t)e;
         bool done = false;
-        for (int c = 0; c < ENV_CHUNK; ++c) {
+        if constexpr (FAST == 2) {
+            const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+            for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
+                if (used >= a.update_cap) {
+                    capped = true;
+                    done = true;
+                    break;
+                }
+                const uint32_t ent = gbuf[c * 64 + lane];
+                const uint32_t i = ent & 0x1FFu;
+                const uint64_t rec = recs[i * a.L.pmax + (ent >> 9)];
+                const uint32_t d = i >> 5, sh = i & 31u;
+                const uint32_t self = P.get(d);
+                const uint32_t y = predictor_apply(P, i, self, rec);
+                const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+                P.put(d, nv);
+                ++used;
+                const uint2 nd = ndelta[i];
+                const bool changed = nv != self;
+                m_lo += changed ? (y ? nd.x : 0u - nd.x) : 0u;
+                m_hi += changed ? (y ? nd.y : 0u - nd.y) : 0u;
+                // :134 the first update is never tested: the check at used == 1 is on o0
+                if (used == 1 ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u) {
+                    done = true;
+                    break;
+                }
+            }
+        } else
+        for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
             if (used >= a.update_cap) {
                 capped = true;
                 done = true;
@@ -406,7 +482,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 changed = table_update_lds(P, i, k53, lds, a.L);
             ++used;
             bool hit;
-            if constexpr (FAST) {
+            if constexpr (FAST == 1) {
                 const uint2 d = ndelta[i];
                 const uint32_t y = P.bit(i);
                 const uint32_t dl = changed ? (y ? d.x : 0u - d.x) : 0u;
@@ -473,6 +549,7 @@ template <int KIND>
 static void* env_fn_w(int W, int replay, int fast) {
 #define PBN_ENV_CASE(w)                                                                  \
     case w:                                                                              \
+        if (fast == 2 && KIND == KIND_PREDICTOR_MIX && !replay) return (void*)k_env<w, KIND_PREDICTOR_MIX, 0, 2>; \
         if (fast) return replay ? (void*)k_env<w, KIND, 1, 1> : (void*)k_env<w, KIND, 0, 1>; \
         return replay ? (void*)k_env<w, KIND, 1, 0> : (void*)k_env<w, KIND, 0, 0>;
     switch (W) {
@@ -562,7 +639,7 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast)
                                               : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast);
     EnvArgs c = a;
-    return launch(fn, grid, env_lds_bytes(W, a.L.bytes), stream, &c, sizeof c);
+    return launch(fn, grid, env_lds_bytes(W, a.L.bytes, replay ? std::min(a.fast, 1) : a.fast), stream, &c, sizeof c);
 }
 
 static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
@@ -582,12 +659,15 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb), blocks_per_cu);
 }
 
-uint32_t env_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK; }
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast) {
+    const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
+    return fast == 2 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES : planes;
+}
 
 int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu) {
     void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast)
                                           : env_fn_w<KIND_PROB_TABLE>(W, 0, fast);
-    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes), blocks_per_cu);
+    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast), blocks_per_cu);
 }
 
 }  // namespace pbn

@@ -88,7 +88,10 @@ struct EnvArgs {
     uint32_t off_ndelta;     // per node: uint2 packed mismatch-counter deltas (fast attractor test)
     unsigned long long* counter;  // work-queue head (zeroed per launch)
     int32_t n_cubes;
-    int32_t fast;            // 1: <= 8 cubes, each caring about <= 255 nodes (byte counters)
+    int32_t fast;            // 1: <= 8 cubes, each caring about <= 255 nodes (byte counters);
+                             // 2: and predictor mix with <= 16 predictors per node, Philox: the
+                             //    draws are generated cooperatively by the whole wave
+    uint32_t off_gen;        // fast == 2: per-wave draw buffers (ENV_GEN_WAVE_BYTES each)
     uint64_t B, env_base, seed;
     uint32_t call_idx, update_cap;
     int32_t A, offset, dedup, horizon, reward_success, action_cost;
@@ -147,7 +150,9 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
 int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu);
-uint32_t env_lds_bytes(int W, uint32_t image_bytes);
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast);
+constexpr uint32_t ENV_CHUNK = 16;          // updates per lane between refill rounds
+constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a);
