@@ -202,6 +202,11 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
                 "traffic_source": pmc_src,
+                # measured HBM-side bytes per launch / launch time: the kernel stores only the
+                # 16-B halves that changed and re-reads a 32 MiB state the 256 MB MALL can hold,
+                # so the algorithmic rate above can exceed the HBM peak
+                "traffic_GBs": (traffic / avg_kernel_s / 1e9) if (traffic and launches) else None,
+                "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if (traffic and launches) else None,
             },
             "node_updates_per_s": value,
             "rollout": rollout,

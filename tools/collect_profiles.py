@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Copy the judged measurement summaries of tools/refresh_profiles.sh from gpurun_out/ into profiles/.
+
+Also writes r01_bench_trace_check.json: the rocprofv3 kernel-trace average of the step kernel over
+the timed launches only (the first --warmup launches excluded), next to bench.py's HIP-event average.
+"""
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+G, P = ROOT / "gpurun_out", ROOT / "profiles"
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+
+lines = [l for l in (G / "bench_full.json").read_text().splitlines() if l.startswith("{")]
+bench = json.loads(lines[-1])
+(P / f"{tag}_bench.json").write_text(json.dumps(bench) + "\n")
+shutil.copy(G / "prof_bench" / "bench_kernel_stats.csv", P / f"{tag}_bench_kernel_stats.csv")
+rows = [r for r in csv.DictReader(open(G / "prof_bench" / "bench_kernel_trace.csv"))
+        if "k_step<4, 1, 1, 0, 1024>" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+w = bench["warmup"]
+check = {"kernel": "pbn::k_step<4, 1, 1, 0, 1024>", "launches": len(d), "warmup_excluded": w,
+         "rocprof_avg_us_timed": sum(d[w:]) / len(d[w:]) / 1e3, "rocprof_avg_us_all": sum(d) / len(d) / 1e3,
+         "bench_hip_event_avg_us": bench["roofline"]["avg_kernel_us"],
+         "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (same defaults as the bench line)"}
+(P / f"{tag}_bench_trace_check.json").write_text(json.dumps(check, indent=1) + "\n")
+shutil.copy(G / "pmc_traffic.json", P / "pmc_traffic.json")
+for k in ("fetch", "write"):
+    src = G / "pmc" / k / "run_counter_collection.csv"
+    if src.exists():
+        shutil.copy(src, P / f"{tag}_pmc_{k}_size.csv")
+shutil.copy(G / "prof_env" / "env_kernel_stats.csv", P / f"{tag}_env_kernel_stats.csv")
+for n in ("r6_131k", "r6_1m"):
+    ls = [l for l in (G / f"{n}.json").read_text().splitlines() if l.startswith("{")]
+    (P / f"{tag}_config5_{n[3:]}.json").write_text(ls[-1] + "\n")
+print(json.dumps(check))
