@@ -356,3 +356,25 @@ def synthetic_truth_table_pbn(n_nodes: int = 200, k: int = 4, seed: int = 0):
         tt = rng.random((2,) * k)
         data.append((mask, tt, f"G{i}", False))
     return data
+
+
+def synthetic_predictor_sets(n_nodes: int, max_preds: int = 5, seed: int = 0, ragged: bool = True):
+    """Random predictor sets in the reference's pickle structure (``predictor_sets.py:45,80-102``).
+
+    Node i gets 1..max_preds predictors (``ragged``) or exactly max_preds, each with 3
+    distinct other nodes as inputs, a positive COD and a random 4x1 coefficient vector.
+    Returns ``(predictor_sets, node_ids)`` for :meth:`PredictorNetwork.from_predictor_sets`.
+    """
+    rng = np.random.default_rng(seed)
+    node_ids = np.arange(1000, 1000 + n_nodes)
+    sets = []
+    for i in range(n_nodes):
+        k = int(rng.integers(1, max_preds + 1)) if ragged else max_preds
+        ps = np.empty((3, k), dtype=object)
+        others = np.array([j for j in range(n_nodes) if j != i])
+        for q in range(k):
+            ps[0, q] = float(rng.uniform(0.05, 1.0))
+            ps[1, q] = rng.normal(size=(4, 1))
+            ps[2, q] = [int(node_ids[j]) for j in rng.choice(others, size=3, replace=False)]
+        sets.append(ps)
+    return sets, node_ids

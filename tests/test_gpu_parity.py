@@ -5,6 +5,8 @@ oracle to finish in seconds; the 1M-env cases check size-independent
 properties (shard invariance, step == rollout, sampled envs vs the oracle).
 """
 
+import zlib
+
 import numpy as np
 import pytest
 
@@ -291,3 +293,67 @@ def test_trajectory_collector_matches_host_api(G):
         assert np.array_equal(buf["n_updates"][t].cpu().numpy().view(np.uint32), nup), t
     assert (flags & 2).all()  # truncated at the horizon == T
     assert np.array_equal(b1.get_state(), b2.get_state())
+
+
+# ----------------------------------------------------------------- env kernel variants vs the oracle
+def _random_cubes(rng, N, H, n_care):
+    cubes = []
+    for _ in range(H):
+        c = ["*"] * N
+        for j in rng.choice(N, size=n_care, replace=False):
+            c[int(j)] = int(rng.integers(0, 2))
+        cubes.append(tuple(c))
+    return cubes
+
+
+@pytest.mark.parametrize("case", ["b28_gen_cap", "b28_h12_general", "b199_nogen", "tt200_fast", "syn500_gen",
+                                  "syn300_wide_cube"])
+def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
+    """Every k_env variant (cooperative draw generation, byte counters without it, general
+    cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs."""
+    from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
+
+    rng = np.random.default_rng(zlib.crc32(case.encode()))
+    cap, A, B = 3000, 3, 1024
+    if case.startswith("b28"):
+        net = load_network("bittner28")
+    elif case == "b199_nogen":
+        net = load_network("bittner199")
+        monkeypatch.setenv("PBNSIM_ENV_NO_GEN", "1")
+    elif case == "tt200_fast":
+        net = load_network("tt200")
+    else:
+        n = 500 if case == "syn500_gen" else 300
+        net = PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(n, 4, seed=n), name=f"syn{n}")
+    N = net.n_nodes
+    if case == "b28_gen_cap":
+        cap = 40
+        attractors = [_random_cubes(rng, N, 2, 5), _random_cubes(rng, N, 2, 5)]
+    elif case == "b28_h12_general":
+        attractors = [_random_cubes(rng, N, 6, 4), _random_cubes(rng, N, 6, 4)]
+    elif case == "syn300_wide_cube":  # one cube caring about 260 > 255 nodes: general matching
+        attractors = [_random_cubes(rng, N, 1, 260) + _random_cubes(rng, N, 2, 3), _random_cubes(rng, N, 1, 3)]
+    else:
+        attractors = [_random_cubes(rng, N, 2, 4), _random_cubes(rng, N, 2, 4)]
+    gnet = G.Net(net)
+    cfg = G.EnvConfig(gnet, attractors, horizon=3)
+    o = oracle_mod.Oracle(net)
+    cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care,
+                target_value=cfg.target_value, horizon=3)
+    b = G.PBNBatch(gnet, B, seed=5, env_id_base=77)
+    b.randomize()
+    st, ns = b.get_state(), np.zeros(B, np.int64)
+    b.set_n_steps(ns)
+    for call in range(3):
+        acts = rng.integers(0, N + 1, size=(B, A)).astype(np.int32)
+        acts[rng.random((B, A)) < 0.5] = 0
+        obs, rew, flags, nup = b.env_step_multi(cfg, acts, update_cap=cap)
+        ref = o.env_step_multi(cfgd, st, ns, acts, seed=5, env_base=77, call_idx=call, update_cap=cap)
+        assert np.array_equal(nup, ref["n_updates"]), case
+        assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), case
+        assert np.array_equal(flags, ref["flags"]), case
+        st, ns = ref["state"], ref["n_steps"]
+        assert np.array_equal(b.get_state(), st), case
+    if case == "b28_gen_cap":
+        assert (flags & 4).any() and not (flags & 4).all()  # some envs capped, some reached an attractor
+    assert (nup > 1).any()
