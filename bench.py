@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--rollout", type=int, default=64, help="updates per launch for the supplementary rollout line")
     p.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
+                        "ranks share one GPU for rehearsals")
     return p.parse_args()
 
 
@@ -95,9 +98,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    device = local if world > 1 else 0
+        ndev = max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local % ndev)
+        dist.init_process_group(args.dist_backend)
+    device = (local % max(torch.cuda.device_count(), 1)) if world > 1 else 0
     if torch.cuda.is_available():
         torch.cuda.set_device(device)
 

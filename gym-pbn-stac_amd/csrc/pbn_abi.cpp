@@ -698,6 +698,7 @@ int pbn_synch_step(pbn_batch* b, uint32_t n_steps, const uint32_t* perturb_gap_t
         HIP_TRY(hipMemcpyAsync(b->s_sync_tab.p, perturb_gap_thr, 4 * (size_t)b->N, hipMemcpyHostToDevice,
                                b->stream));
         a.gap_thr = (const uint32_t*)b->s_sync_tab.p;
+        a.gap_inv_log2 = gap_inv_log2(perturb_gap_thr, b->N);
     }
     a.lds_bytes = sync_layout(b->W, b->net->L.bytes, b->N, &a);
     if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "sync LDS footprint %u B too large", a.lds_bytes);
@@ -748,6 +749,7 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     a.n_targets = n_targets;
     a.targets = d_tgt;
     a.gap_thr = flip_gap_thr ? d_gap : nullptr;
+    a.gap_inv_log2 = flip_gap_thr ? gap_inv_log2(flip_gap_thr, b->N) : 0.0f;
     a.hist = (uint64_t*)b->s_ssd_hist.p;
     a.lds_bytes = ssd_layout(b->W, b->net->L.bytes, b->N, n_targets, &a);
     if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "SSD LDS footprint %u B too large", a.lds_bytes);

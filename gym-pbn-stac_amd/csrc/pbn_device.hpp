@@ -226,13 +226,45 @@ __device__ __forceinline__ uint32_t table_update_lds(const P_t& P, uint32_t i, u
     return nv != self;
 }
 
+// gap(u) = #{k >= 1 : u < T_k} for the non-increasing table gap[k-1] = T_k = floor((1-p)^k 2^32).
+// T_k > u  <=>  k <= log((u+1) 2^-32) / log(1-p), so a float estimate e of that bound is within
+// one of the answer; three table entries around e settle it (one LDS round trip), and a result
+// that fails the bracket check -- only if the estimate was off by more than one -- falls back to
+// a binary search. inv_log2q = 1 / log2(1-p) (from the table, host side); 0 when p == 1.
+__device__ __forceinline__ uint32_t geo_gap(uint32_t u, const uint32_t* gap, uint32_t N, float inv_log2q) {
+    const float x = ((float)u + 1.0f) * 2.3283064365386963e-10f;
+    const float L = __log2f(x) * inv_log2q;
+    const uint32_t e = L >= (float)N ? N : (uint32_t)fmaxf(L, 0.0f);
+    // gt(k) = "T_k > u", with T_0 = +inf and T_k = 0 past N
+    auto rd = [&](uint32_t k) -> uint32_t { return (k >= 1 && k <= N) ? gap[k - 1] : 0u; };
+    const uint32_t vm = rd(e - 1), v0 = rd(e), v1 = rd(e + 1), v2 = rd(e + 2);
+    const bool bm = e == 1 || (e >= 2 && vm > u);
+    const bool b0 = e == 0 || v0 > u;
+    const bool b1 = e + 1 <= N && v1 > u;
+    const bool b2 = e + 2 <= N && v2 > u;
+    const uint32_t g = e + (b1 ? 1u : 0u) - (b0 ? 0u : 1u);  // e - 1, e or e + 1
+    const bool bg = g == e + 1 ? b1 : (g == e ? b0 : bm);
+    const bool bg1 = g == e + 1 ? b2 : (g == e ? b1 : b0);
+    if (bg && !bg1) return g;  // T_g > u >= T_{g+1}: g is the count
+    uint32_t lo = 0, hi = N;  // largest k in [0, N] with u < T_k
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (u < gap[mid - 1])
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
 // Independent Bernoulli(p) events over positions [0, N) generated as successive
 // geometric gaps: gap = #{k >= 1 : u < T_k}, T_k = floor((1-p)^k 2^32) (LDS table
 // gap[0..N-1] = T_1..T_N), u = 32-bit Philox words from ctr {c0, m, gid, stream}
 // with m = 0, 1, ... Calls on_pos(pos) for every event position in increasing order.
 template <class F>
 __device__ __forceinline__ void bernoulli_positions(uint64_t seed, uint32_t c0, uint32_t stream, uint64_t gid,
-                                                    const uint32_t* gap, uint32_t N, F&& on_pos) {
+                                                    const uint32_t* gap, uint32_t N, float inv_log2q,
+                                                    F&& on_pos) {
     uint32_t w[4];
     uint32_t m = 0, wi = 4, pos = 0;
     bool first = true;
@@ -241,15 +273,7 @@ __device__ __forceinline__ void bernoulli_positions(uint64_t seed, uint32_t c0, 
             philox_draw(seed, c0, m++, gid, stream, w);
             wi = 0;
         }
-        const uint32_t u = w[wi++];
-        uint32_t lo = 0, hi = N;  // largest k in [0, N] with u < T_k (T_0 = +inf)
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (u < gap[mid - 1])
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
+        const uint32_t lo = geo_gap(w[wi++], gap, N, inv_log2q);
         pos = first ? lo : pos + 1u + lo;
         first = false;
         if (pos >= N) break;

@@ -100,7 +100,15 @@ struct EnvArgs {
     const uint64_t* draws_k;
 };
 
-constexpr uint32_t MT_ROW = 624;  // u32 words of one MT19937 state row
+constexpr uint32_t MT_ROW = 624;
+
+// 1 / log2(1-p) from a geometric-gap table T_k = floor((1-p)^k 2^32) (host side): taken at the
+// largest k whose T_k keeps >= 20 significant bits; 0 when every T_k is tiny (p ~ 1).
+inline float gap_inv_log2(const uint32_t* T, int N) {
+    for (int k = N; k >= 1; --k)
+        if (T[k - 1] >= (1u << 20)) return (float)((double)k / __builtin_log2((double)T[k - 1] / 4294967296.0));
+    return 0.0f;
+}  // u32 words of one MT19937 state row
 
 struct MTArgs {
     uint64_t* state;        // [B][W]
@@ -127,6 +135,7 @@ struct SSDArgs {
     int32_t n_targets;         // g <= 12 (2^g LDS bins)
     const int32_t* targets;    // [g] node indices, first = most significant bucket bit
     const uint32_t* gap_thr;   // [N] T_k = floor((1-p)^k 2^32), k = 1..N; null = no flips
+    float gap_inv_log2;        // 1 / log2(1-p) estimated from the table (geo_gap's first guess)
     uint64_t* hist;            // [2^g] accumulated counts (device)
     uint32_t off_planes, off_gap, off_tbit, off_targets, off_hist, lds_bytes;
 };
@@ -139,6 +148,7 @@ struct SyncArgs {
     uint64_t step_base;       // synchronous-step counter of the first step (Philox)
     uint32_t T;
     const uint32_t* gap_thr;  // [N] perturbation gap table (T_k = floor((1-p)^k 2^32)); null = off
+    float gap_inv_log2;       // 1 / log2(1-p) estimated from the table
     uint32_t off_planes, off_gap, lds_bytes;
 };
 

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd(SSDArgs a) {
             ++run;
             // independent Bernoulli(p) flips (eval.py:92-95) as geometric gaps
             if (a.gap_thr)
-                bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, [&](uint32_t pos) {
+                bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2, [&](uint32_t pos) {
                     const uint32_t d = pos >> 5, sh = pos & 31u;
                     P.put(d, P.get(d) ^ (1u << sh));
                     const int tb = tbit[pos];

@@ -41,7 +41,7 @@ __global__ __launch_bounds__(BLOCK) void k_sync(SyncArgs a) {
             const uint64_t st = a.step_base + t;
             bool flipped = false;
             if (a.gap_thr)
-                bernoulli_positions(a.seed, (uint32_t)st, STREAM_SYNC_PERT, g, gap, N, [&](uint32_t pos) {
+                bernoulli_positions(a.seed, (uint32_t)st, STREAM_SYNC_PERT, g, gap, N, a.gap_inv_log2, [&](uint32_t pos) {
                     const uint32_t d = pos >> 5;
                     P0.put(d, P0.get(d) ^ (1u << (pos & 31u)));
                     flipped = true;
