@@ -26,8 +26,12 @@ def __getattr__(name):
         from . import batch
 
         return getattr(batch, name)
-    if name in ("Graph", "PBN", "PBNTargetMultiEnv", "VecPBNTargetMultiEnv", "PBNEnv", "state_to_idx"):
+    if name in ("Graph", "PBN", "PBNTargetEnv", "PBNTargetMultiEnv", "VecPBNTargetMultiEnv", "PBNEnv", "state_to_idx"):
         from . import envs
 
         return getattr(envs, name)
+    if name == "make":
+        from .registry import make
+
+        return make
     raise AttributeError(name)

@@ -2,6 +2,7 @@
 
 * :class:`Graph`            -- ``gym_PBN/envs/bittner/base.py`` ``Graph`` (step/flipNode/setState/getState/...).
 * :class:`PBN`              -- ``gym_PBN/envs/common/pbn.py`` ``PBN`` (reset/flip/step/state).
+* :class:`PBNTargetEnv`     -- ``gym_PBN/envs/pbn_target.py`` single-flip target env (R5, intended semantics).
 * :class:`PBNTargetMultiEnv` -- ``gym_PBN/envs/pbn_target_multi.py`` single env (reset/step, R6).
 * :class:`VecPBNTargetMultiEnv` -- the same MDP over B envs in one call (Stable-Baselines3 VecEnv shaped).
 * :class:`PBNEnv`           -- ``gym_PBN/envs/pbn_env.py`` ``PBNEnv`` step/reward conventions (R7).
@@ -235,6 +236,84 @@ class PBNTargetMultiEnv:
         return o, int(rew[0]), bool(flags[0] & L.FLAG_TERMINATED), bool(flags[0] & L.FLAG_TRUNCATED), info
 
 
+def _cube_match(cube, state) -> bool:
+    return all(c == "*" or int(c) == int(x) for c, x in zip(cube, state))
+
+
+class PBNTargetEnv:
+    """``PBNTargetEnv`` (``pbn_target.py:241-352``, the ``Bittner-N-v0`` envs) -- R5.
+
+    ``step`` raises at HEAD in both modes, so this follows the intended
+    semantics, build-defined: flip node ``action - 1`` (0 = none), one R1 update
+    (``force=True``) or updates until the state is attracting (``force=False``, the
+    ``is_attracting_state`` loop); reward +20 and terminated when the state matches a
+    cube of the target attractor (``in_target`` :289-301, '*' = any), else -5;
+    ``truncated = n_steps == horizon``. ``reset`` draws two distinct attractors
+    (``random.sample``, :333) and fills '*' bits with ``randint(0, 1)`` (:334-341).
+    Transitions run on the GPU (Philox); host draws come from a per-env ``random.Random``.
+    """
+
+    def __init__(self, network, all_attractors, horizon: int = 100, device: int = 0, seed: int = 0,
+                 update_cap: int = 1 << 20, name: Optional[str] = None):
+        self.graph = Graph(network, device=device, seed=seed)
+        self.N = self.graph.N
+        self.name = name or self.graph.network.name
+        self.all_attractors = [list(a) for a in all_attractors]
+        self.cubes = [c for a in self.all_attractors for c in a]
+        self.horizon = int(horizon)
+        self.update_cap = int(update_cap)
+        self.n_steps = 0
+        self.target = None
+        self._rng = random.Random()
+
+    def _seed(self, seed):  # pbn_target.py:205-207
+        self._rng.seed(seed)
+
+    def is_attracting_state(self, state) -> bool:
+        return any(_cube_match(c, state) for c in self.cubes)
+
+    def in_target(self, observation) -> bool:  # :289-301
+        if self.target is None:
+            raise ValueError("Target should have been initialized during env.reset()")
+        return any(_cube_match(c, observation) for c in self.target)
+
+    def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):  # :328-352
+        if seed:  # `if seed:` -- seed 0 is not applied (Q9)
+            self._seed(seed)
+        state_attractor, target_attractor = self._rng.sample(self.all_attractors, 2)
+        state = list(self._rng.choice(state_attractor))
+        target = list(self._rng.choice(target_attractor))
+        for i in range(len(state)):
+            if state[i] == "*":
+                state[i] = self._rng.randint(0, 1)
+            if target[i] == "*":
+                target[i] = self._rng.randint(0, 1)
+        self.graph.setState(state)
+        self.n_steps = 0
+        obs = self.graph.getState()
+        self.target = target_attractor
+        return (tuple(state), tuple(target)), {"observation_idx": state_to_idx(obs), "observation_dict": obs}
+
+    def step(self, action: int = 0, force: bool = True):
+        if not (0 <= int(action) <= self.N):
+            raise Exception(f"Invalid action {action}, not in action space.")
+        self.n_steps += 1
+        if action != 0:
+            self.graph.flipNode(int(action) - 1)
+        obs = self.graph.step()
+        n = 1
+        while not force and not self.is_attracting_state(obs):
+            if n >= self.update_cap:
+                raise RuntimeError(f"update cap ({self.update_cap}) reached before an attracting state")
+            obs = self.graph.step()
+            n += 1
+        terminated = self.in_target(obs)
+        reward = 20 if terminated else -5  # :303-326
+        truncated = self.n_steps == self.horizon
+        return np.array(obs), reward, terminated, truncated, {"observation_idx": state_to_idx(obs),
+                                                              "observation_dict": obs, "n_updates": n}
+
+
 class PBNEnv:
     """``PBNEnv`` (``pbn_env.py``) over the device truth-table engine (R7).
 
@@ -340,4 +419,5 @@ class PBNEnv:
         return observation, reward, terminated, truncated, {"observation_idx": self._state_to_idx(observation)}
 
 
-__all__ = ["Graph", "PBN", "PBNTargetMultiEnv", "VecPBNTargetMultiEnv", "PBNEnv", "state_to_idx", "pack_bits"]
+__all__ = ["Graph", "PBN", "PBNTargetEnv", "PBNTargetMultiEnv", "VecPBNTargetMultiEnv", "PBNEnv", "state_to_idx",
+           "pack_bits"]

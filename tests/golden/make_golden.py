@@ -308,6 +308,37 @@ def gen_r6(base, multi, name, n_fixed, horizon, seeds, n_steps, list_every=0, ma
           "terminated", int(out["terminated"].sum()), "truncated", int(out["truncated"].sum()))
 
 
+def gen_r5_reset(base):
+    """R5 reset KAT: PBNTargetEnv.reset (pbn_target.py:328-352) -- reset works at HEAD, step does not."""
+    tgt = refload.load_target_env()
+    net = load_network("bittner28")
+    ps = load_pickle_safely(BITTNER / PICKLES["bittner28"])
+    g = refload.build_graph(base, ps, net.node_ids)
+    env = object.__new__(tgt.PBNTargetEnv)
+    env.graph = g
+    env.horizon = 100
+    N = net.n_nodes
+    rng = np.random.default_rng(3)
+    atts = []
+    for a in range(4):
+        cubes = []
+        for _ in range(1 + a % 2):
+            c = ["*"] * N
+            for j in rng.choice(N, size=10, replace=False):
+                c[int(j)] = int(rng.integers(0, 2))
+            cubes.append(tuple(c))
+        atts.append(cubes)
+    env.all_attractors = atts
+    cases = []
+    for seed in (1, 2, 3, 11, 12345):
+        (st, tg), info = env.reset(seed=seed)
+        cases.append({"seed": seed, "state": list(st), "target": list(tg), "graph": [int(x) for x in g.getState()],
+                      "target_attractor": [list(c) for c in env.target]})
+    doc = {"attractors": [[list(c) for c in a] for a in atts], "cases": cases}
+    (HERE / "r5_reset_kat.json").write_text(json.dumps(doc) + "\n")
+    print("r5 reset kat", len(cases))
+
+
 def gen_cabean_kat(multi):
     """KAT: parse_attractors(sample_cabean_out) (get_attractors_from_cabean.py:57-81)."""
     cab = sys.modules["gym_PBN.utils.get_attractors_from_cabean"]
@@ -505,6 +536,8 @@ def main():
         gen_r6(base, multi, "bittner28", n_fixed=16, horizon=7, seeds=(1, 2, 3), n_steps=40, list_every=5)
         gen_r6(base, multi, "bittner199", n_fixed=165, horizon=100, seeds=(4, 5), n_steps=10)
     gen_cabean_kat(multi)
+    if not only or "r5" in only:
+        gen_r5_reset(base)
 
 
 if __name__ == "__main__":

@@ -130,6 +130,12 @@ def load_multi_env():
                  package="gym_PBN.envs")
 
 
+def load_target_env():
+    """Return the reference ``pbn_target`` module (R5; its ``step`` raises at HEAD, ``reset`` runs)."""
+    load_multi_env()
+    return _load("gym_PBN.envs.pbn_target", PKG / "envs" / "pbn_target.py", package="gym_PBN.envs")
+
+
 def load_mdp_envs():
     """Return the reference modules (pbn_env, pbcn_env, sampled_data, self_triggering, pbcn)."""
     load_hot_path()

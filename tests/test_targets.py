@@ -1,0 +1,51 @@
+"""R5 single-flip target env (pbn_target.py, intended semantics) and the env-id registry."""
+
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+KAT = json.loads((GOLDEN / "r5_reset_kat.json").read_text())
+
+
+def _atts():
+    return [[tuple(x if x == "*" else int(x) for x in c) for c in a] for a in KAT["attractors"]]
+
+
+def test_registry_ids_and_required_inputs():
+    from gym_pbn_amd.registry import REGISTRY, make
+
+    for i in ("gym-PBN/PBN-v0", "gym-PBN/PBCN-self-triggering-v0", "gym-PBN/Bittner-28-v0",
+              "gym-PBN/BittnerMulti-28-v0", "gym-PBN/BittnerMulti-30-v0", "gym-PBN/BittnerMultiGeneral-v0"):
+        assert i in REGISTRY
+    with pytest.raises(KeyError):
+        make("gym-PBN/Nope-v0")
+    with pytest.raises(ValueError):
+        make("gym-PBN/BittnerMulti-28-v0")  # attractors come from cabean: required
+    with pytest.raises(NotImplementedError):
+        make("gym-PBN/BittnerMulti-7-v0", all_attractors=[[("*",) * 7]])  # network needs xls inference
+
+
+@pytest.mark.gpu
+def test_target_env_reset_matches_reference_and_step_semantics():
+    from gym_pbn_amd.registry import make
+
+    env = make("gym-PBN/Bittner-28-v0", all_attractors=_atts(), horizon=3, seed=4)
+    for case in KAT["cases"]:
+        (st, tg), info = env.reset(seed=case["seed"])
+        assert list(st) == case["state"] and list(tg) == case["target"], case["seed"]
+        assert list(env.graph.getState()) == case["graph"]
+        assert [list(c) for c in env.target] == case["target_attractor"]
+    env.reset(seed=1)
+    s0 = np.array(env.graph.getState())
+    for t in range(3):
+        obs, r, term, trunc, info = env.step(5)  # flip node 4, one update (force=True)
+        assert (obs != s0).sum() <= 2 and r in (20, -5) and term == (r == 20)
+        assert trunc == (t == 2)
+        s0 = obs
+    with pytest.raises(Exception):
+        env.step(29)
+    obs, r, term, trunc, info = env.step(0, force=False)  # until attracting
+    assert env.is_attracting_state(obs) and info["n_updates"] >= 1
