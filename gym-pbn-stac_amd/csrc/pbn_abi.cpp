@@ -94,7 +94,7 @@ struct pbn_envcfg {
     uint32_t off_cubes = 0, off_target = 0, off_ndelta = 0;
     int fast = 0;
     std::vector<uint64_t> reset_care, reset_value;
-    int32_t horizon = 100, reward_success = 1000, action_cost = 1;
+    int32_t horizon = 100, reward_success = 1000, action_cost = 1, first_tested = 0;
     std::mutex mu;
     struct Dev {
         void* image = nullptr;
@@ -840,6 +840,7 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
     c->horizon = d->horizon;
     c->reward_success = d->reward_success;
     c->action_cost = d->action_cost;
+    c->first_tested = d->first_update_tested ? 1 : 0;
     *out = c;
     return 0;
 }
@@ -937,6 +938,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.horizon = cfg->horizon;
     a.reward_success = cfg->reward_success;
     a.action_cost = cfg->action_cost;
+    a.first_tested = cfg->first_tested;
     a.draw_off = (const int64_t*)d_off;
     a.draws_i = (const uint32_t*)d_di;
     a.draws_k = (const uint64_t*)d_dk;

@@ -446,7 +446,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 m_lo += changed ? (y ? nd.x : 0u - nd.x) : 0u;
                 m_hi += changed ? (y ? nd.y : 0u - nd.y) : 0u;
                 // :134 the first update is never tested: the check at used == 1 is on o0
-                if (used == 1 ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u) {
+                if ((used == 1 && !a.first_tested) ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u) {
                     done = true;
                     break;
                 }
@@ -490,9 +490,10 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 m_lo += dl;
                 m_hi += dh;
                 // :134 the first update is never tested: the check at used == 1 is on o0
-                hit = used == 1 ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
+                hit = (used == 1 && !a.first_tested) ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
             } else {
-                hit = (used == 1) ? hit0 : ((changed || used == 2) && attracting_plane<W>(P, cubes, H));
+                hit = (used == 1) ? (a.first_tested ? attracting_plane<W>(P, cubes, H) : hit0)
+                                  : ((changed || used == 2) && attracting_plane<W>(P, cubes, H));
             }
             if (hit) {
                 done = true;
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         from_plane<W>(P, s);
         uint64_t o[W];
 #pragma unroll
-        for (int k = 0; k < W; ++k) o[k] = used <= 1 ? o0[k] : s[k];
+        for (int k = 0; k < W; ++k) o[k] = (used <= 1 && !a.first_tested) ? o0[k] : s[k];
         const uint64_t eu = (uint64_t)e;
         store_state<W>(a.state + eu * W, s);
         store_state<W>(a.obs + eu * W, o);

@@ -95,6 +95,7 @@ struct EnvArgs {
     uint64_t B, env_base, seed;
     uint32_t call_idx, update_cap;
     int32_t A, offset, dedup, horizon, reward_success, action_cost;
+    int32_t first_tested;     // 1: test the state after the first update too (pbn_target.py R5)
     const int64_t* draw_off;  // replay mode: [B+1]
     const uint32_t* draws_i;
     const uint64_t* draws_k;

@@ -71,6 +71,7 @@ class EnvCfgDesc(C.Structure):
         ("n_reset_cubes", C.c_int32), ("reset_care", _u64p), ("reset_value", _u64p),
         ("target_care", _u64p), ("target_value", _u64p),
         ("horizon", C.c_int32), ("reward_success", C.c_int32), ("action_cost", C.c_int32),
+        ("first_update_tested", C.c_int32),
     ]
 
 

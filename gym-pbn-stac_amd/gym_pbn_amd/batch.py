@@ -97,7 +97,8 @@ class EnvConfig:
     target is ``attractors[-1][0]`` (``in_target`` only tests ``target[0]``).
     """
 
-    def __init__(self, net: Net, attractors, horizon: int = 100, reward_success: int = 1000, action_cost: int = 1):
+    def __init__(self, net: Net, attractors, horizon: int = 100, reward_success: int = 1000, action_cost: int = 1,
+                 first_update_tested: bool = False):
         self.net = net
         N, W = net.n_nodes, net.n_words
         self.attractors = [list(a) for a in attractors]
@@ -125,6 +126,8 @@ class EnvConfig:
         d.horizon = self.horizon
         d.reward_success = self.reward_success
         d.action_cost = self.action_cost
+        self.first_update_tested = bool(first_update_tested)
+        d.first_update_tested = int(self.first_update_tested)
         h = C.c_void_p()
         L.check(L.lib.pbn_envcfg_create(net.handle, C.byref(d), C.byref(h)))
         self._h = h

@@ -265,6 +265,9 @@ class PBNTargetEnv:
         self.n_steps = 0
         self.target = None
         self._rng = random.Random()
+        # force=False runs in the until-attractor kernel, testing the state after every update
+        self._cfg = EnvConfig(self.graph._b.net, self.all_attractors, horizon=self.horizon,
+                              first_update_tested=True)
 
     def _seed(self, seed):  # pbn_target.py:205-207
         self._rng.seed(seed)
@@ -298,15 +301,20 @@ class PBNTargetEnv:
         if not (0 <= int(action) <= self.N):
             raise Exception(f"Invalid action {action}, not in action space.")
         self.n_steps += 1
-        if action != 0:
-            self.graph.flipNode(int(action) - 1)
-        obs = self.graph.step()
-        n = 1
-        while not force and not self.is_attracting_state(obs):
-            if n >= self.update_cap:
-                raise RuntimeError(f"update cap ({self.update_cap}) reached before an attracting state")
+        if not self.graph._initialised:
+            raise Exception("Forgot to initialise the states")
+        if force:
+            if action != 0:
+                self.graph.flipNode(int(action) - 1)
             obs = self.graph.step()
-            n += 1
+            n = 1
+        else:  # flip + updates until attracting, in one kernel call
+            words, _, flags, nup = self.graph._b.env_step_multi(self._cfg, np.array([[int(action)]], np.int32),
+                                                                offset=1, dedup=True, update_cap=self.update_cap)
+            if flags[0] & L.FLAG_CAPPED:
+                raise RuntimeError(f"update cap ({self.update_cap}) reached before an attracting state")
+            obs = tuple(int(x) for x in unpack_bits(words, self.N)[0])
+            n = int(nup[0])
         terminated = self.in_target(obs)
         reward = 20 if terminated else -5  # :303-326
         truncated = self.n_steps == self.horizon

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 1
+#define PBN_ABI_VERSION 2
 
 enum {
     PBN_OK = 0,
@@ -102,6 +102,10 @@ typedef struct {
     int32_t horizon;              /* truncated = n_steps == horizon (:224) */
     int32_t reward_success;       /* +1000 (:218-219) */
     int32_t action_cost;          /* 1 per unique action value (:222) */
+    /* 0: the first update's result is never tested -- the test after it is on the pre-update
+     *    snapshot (PBNTargetMultiEnv, :133-134);
+     * 1: the state after every update is tested (PBNTargetEnv.step(force=False), pbn_target.py:267-271). */
+    int32_t first_update_tested;
 } pbn_envcfg_desc;
 
 /* flags returned per env by pbn_env_step_multi* */

@@ -343,6 +343,7 @@ typedef struct {
     const uint64_t *value; /* [H][W] */
     const uint64_t *target_care, *target_value; /* [W]: all_attractors[-1][0] */
     int horizon, reward_success, action_cost;
+    int first_tested; /* 1: PBNTargetEnv.step(force=False) -- the state after update 1 is tested too */
 } orc_envcfg;
 
 static inline int cube_match(const uint64_t *s, const uint64_t *care, const uint64_t *val, int W) {
@@ -422,7 +423,7 @@ EXPORT int orc_env_step_multi(const orc_net *n, const orc_envcfg *c, uint64_t *s
             node_update(n, s, i, k53);
             used++;
             /* :134 the first update is never tested; :135-146 loop until obs is attracting */
-            if (used == 1) {
+            if (used == 1 && !c->first_tested) {
                 if (attracting(c, o, W)) break;
             } else {
                 memcpy(o, s, 8 * (size_t)W);

@@ -307,7 +307,8 @@ def _random_cubes(rng, N, H, n_care):
 
 
 @pytest.mark.parametrize("case", ["b28_gen_cap", "b28_h12_general", "b199_nogen", "tt200_fast", "syn500_gen",
-                                  "syn300_wide_cube"])
+                                  "syn300_wide_cube", "b28_first_tested", "b28_h12_first_tested",
+                                  "tt200_first_tested"])
 def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     """Every k_env variant (cooperative draw generation, byte counters without it, general
     cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs."""
@@ -315,12 +316,13 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
 
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     cap, A, B = 3000, 3, 1024
+    first = case.endswith("first_tested")  # PBNTargetEnv.step(force=False) semantics
     if case.startswith("b28"):
         net = load_network("bittner28")
     elif case == "b199_nogen":
         net = load_network("bittner199")
         monkeypatch.setenv("PBNSIM_ENV_NO_GEN", "1")
-    elif case == "tt200_fast":
+    elif case.startswith("tt200"):
         net = load_network("tt200")
     else:
         n = 500 if case == "syn500_gen" else 300
@@ -329,17 +331,17 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     if case == "b28_gen_cap":
         cap = 40
         attractors = [_random_cubes(rng, N, 2, 5), _random_cubes(rng, N, 2, 5)]
-    elif case == "b28_h12_general":
+    elif case.startswith("b28_h12"):
         attractors = [_random_cubes(rng, N, 6, 4), _random_cubes(rng, N, 6, 4)]
     elif case == "syn300_wide_cube":  # one cube caring about 260 > 255 nodes: general matching
         attractors = [_random_cubes(rng, N, 1, 260) + _random_cubes(rng, N, 2, 3), _random_cubes(rng, N, 1, 3)]
     else:
         attractors = [_random_cubes(rng, N, 2, 4), _random_cubes(rng, N, 2, 4)]
     gnet = G.Net(net)
-    cfg = G.EnvConfig(gnet, attractors, horizon=3)
+    cfg = G.EnvConfig(gnet, attractors, horizon=3, first_update_tested=first)
     o = oracle_mod.Oracle(net)
     cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care,
-                target_value=cfg.target_value, horizon=3)
+                target_value=cfg.target_value, horizon=3, first_tested=first)
     b = G.PBNBatch(gnet, B, seed=5, env_id_base=77)
     b.randomize()
     st, ns = b.get_state(), np.zeros(B, np.int64)

@@ -32,7 +32,7 @@ def test_registry_ids_and_required_inputs():
 def test_target_env_reset_matches_reference_and_step_semantics():
     from gym_pbn_amd.registry import make
 
-    env = make("gym-PBN/Bittner-28-v0", all_attractors=_atts(), horizon=3, seed=4)
+    env = make("gym-PBN/Bittner-28-v0", all_attractors=_atts(), horizon=3, seed=4, update_cap=1 << 22)
     for case in KAT["cases"]:
         (st, tg), info = env.reset(seed=case["seed"])
         assert list(st) == case["state"] and list(tg) == case["target"], case["seed"]
@@ -47,5 +47,13 @@ def test_target_env_reset_matches_reference_and_step_semantics():
         s0 = obs
     with pytest.raises(Exception):
         env.step(29)
-    obs, r, term, trunc, info = env.step(0, force=False)  # until attracting
-    assert env.is_attracting_state(obs) and info["n_updates"] >= 1
+    # until attracting (force=False) on the R6 fixture's attractors (reached within ~40k updates there)
+    from conftest import cubes_to_attractors, golden
+
+    easy = cubes_to_attractors(golden("r6_bittner28.npz"), 28)
+    env2 = make("gym-PBN/Bittner-28-v0", all_attractors=easy, horizon=50, seed=9, update_cap=1 << 22)
+    env2.reset(seed=5)
+    for _ in range(5):
+        obs, r, term, trunc, info = env2.step(int(np.random.default_rng(_).integers(0, 29)), force=False)
+        assert env2.is_attracting_state(obs) and info["n_updates"] >= 1
+        assert r == (20 if env2.in_target(obs) else -5)
