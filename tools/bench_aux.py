@@ -7,6 +7,7 @@
 * synchronous step (``Graph.synch_step``, base.py:286-303): 1M envs x 20 steps, perturbation
   p=0.001 (base.py:191) -> node-updates/s (N updates per env-step).
 * MT mode (seed-only parity): 65,536 envs x 2,000 R1 updates.
+* BASELINE config 2 (Bittner-28, 65,536 envs): step mode and rollout (256 updates per launch).
 
 Prints one JSON line. Timing: HIP events over the region (``PBNBatch.timing(2)``).
 """
@@ -65,6 +66,21 @@ def main():
     b.mt_seed(np.arange(B, dtype=np.uint64))
     s, wall, _ = timed(b, lambda: b.mt_step(T))
     out["mt_step"] = {"envs": B, "updates": T, "s": s, "node_updates_per_s": B * T / s}
+    b.close()
+    # BASELINE config 2: Bittner-28, 65,536 envs (state 512 KiB: launch-bound in step mode)
+    n28 = Net(load_network("bittner28"))
+    b = PBNBatch(n28, 1 << 16, seed=5)
+    b.randomize()
+
+    def steps28():
+        for _ in range(200):
+            b.step(1)
+
+    s, wall, n = timed(b, steps28)
+    s2, _, n2 = timed(b, lambda: b.rollout(256))
+    out["bittner28_64k"] = {"envs": 1 << 16, "step_us_per_launch": s / n * 1e6,
+                            "step_env_steps_per_s": (1 << 16) * n / s,
+                            "rollout256_node_updates_per_s": (1 << 16) * 256 * n2 / s2}
     b.close()
     B = 8 << 20
     b = PBNBatch(net, B, seed=4)
