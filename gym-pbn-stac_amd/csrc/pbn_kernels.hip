@@ -76,21 +76,6 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             uint64_t(&s)[W] = h ? nxt : cur;
             const uint32_t i = h ? i1 : i0;
             const uint32_t d = i >> 5, sh = i & 31u;
-#ifdef PBN_STEP_REG_BITS
-            if constexpr (KIND == KIND_PREDICTOR_MIX) {  // measurement variant: bits from registers
-                const uint64_t rec = h ? r1 : r0;
-                const uint32_t sf = getbit<W>(s, i);
-                const uint32_t p = (getbit<W>(s, (uint32_t)rec & 0xFFFFu) << 3) |
-                                   (getbit<W>(s, (uint32_t)(rec >> 16) & 0xFFFFu) << 2) |
-                                   (getbit<W>(s, (uint32_t)(rec >> 32) & 0xFFFFu) << 1) | sf;
-                const uint32_t yy = (uint32_t)(rec >> (48 + p)) & 1u;
-                if (yy != sf) {
-                    setbit<W>(s, i, yy);
-                    store_dirty<W>(a.state + eh * W, s, 1u << (i >> 6));
-                }
-                continue;
-            }
-#endif
             to_plane<W>(P, s);
             const uint32_t self = P.get(d);
             uint32_t y;
