@@ -110,21 +110,6 @@ __device__ __forceinline__ void store_state(uint64_t* __restrict__ p, const uint
     }
 }
 
-// Store only the 16-byte pairs (8-byte words for odd W) whose dirty bit is set.
-template <int W>
-__device__ __forceinline__ void store_dirty(uint64_t* __restrict__ p, const uint64_t (&s)[W], uint32_t dirty) {
-    if constexpr (W % 2 == 0) {
-        ulonglong2* q = reinterpret_cast<ulonglong2*>(p);
-#pragma unroll
-        for (int k = 0; k < W / 2; ++k)
-            if (dirty & (3u << (2 * k))) q[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < W; ++k)
-            if (dirty & (1u << k)) p[k] = s[k];
-    }
-}
-
 // ---------------------------------------------------------------- LDS staging
 // Copy the network image (16-byte granules) into LDS; every thread participates.
 __device__ __forceinline__ void stage_image(const uint4* __restrict__ img, uint32_t n16, uint4* lds) {
