@@ -88,13 +88,7 @@ __device__ __forceinline__ void load_state(const uint64_t* __restrict__ p, uint6
         const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
 #pragma unroll
         for (int k = 0; k < W / 2; ++k) {
-#ifdef PBN_EXP_NT_LOAD
-            ulonglong2 v;
-            v.x = __builtin_nontemporal_load(&q[k].x);
-            v.y = __builtin_nontemporal_load(&q[k].y);
-#else
             ulonglong2 v = q[k];
-#endif
             s[2 * k] = v.x;
             s[2 * k + 1] = v.y;
         }
@@ -109,14 +103,7 @@ __device__ __forceinline__ void store_state(uint64_t* __restrict__ p, const uint
     if constexpr (W % 2 == 0) {
         ulonglong2* q = reinterpret_cast<ulonglong2*>(p);
 #pragma unroll
-        for (int k = 0; k < W / 2; ++k) {
-#ifdef PBN_EXP_NT_STORE
-            __builtin_nontemporal_store(s[2 * k], &q[k].x);
-            __builtin_nontemporal_store(s[2 * k + 1], &q[k].y);
-#else
-            q[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
-#endif
-        }
+        for (int k = 0; k < W / 2; ++k) q[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
     } else {
 #pragma unroll
         for (int k = 0; k < W; ++k) p[k] = s[k];
