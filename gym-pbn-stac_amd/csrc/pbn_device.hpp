@@ -148,6 +148,7 @@ __device__ __forceinline__ uint32_t predictor_choice(uint32_t i, uint64_t k53, c
                                                      const NetLayout& L) {
     const ulonglong2* thr = reinterpret_cast<const ulonglong2*>(tbl + L.off_thr) + (i * L.tp >> 1);
     uint32_t j = 0;
+#pragma unroll 4  // several independent 16-B reads in flight (Bittner-28: 7 per update)
     for (uint32_t q = 0; q < (L.tp >> 1); ++q) {
         const ulonglong2 t = thr[q];
         j += (k53 >= t.x ? 1u : 0u) + (k53 >= t.y ? 1u : 0u);
