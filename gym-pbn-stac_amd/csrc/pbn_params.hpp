@@ -19,7 +19,7 @@ enum { STORE_FULL = 0, STORE_DIRTY = 1 };
 
 constexpr int BLOCK = 256;          // 4 wave64 per workgroup
 constexpr int MAX_WORDS = 8;        // N <= 512
-constexpr uint32_t MAX_IMAGE = 48 * 1024;  // LDS bytes for the network image (+ 16 KiB state planes)
+constexpr uint32_t MAX_IMAGE = 48 * 1024;  // LDS bytes for the network image (state planes come on top)
 
 // Byte offsets of the tables inside the LDS image (16-byte aligned image).
 // Predictor-mix networks use a padded per-node layout so that both table reads of an

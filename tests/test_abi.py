@@ -33,7 +33,8 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(_lib.lib, name), name
         assert name in _lib.SIGNATURES, f"{name} missing from the ctypes signature table"
-    assert _lib.lib.pbn_abi_version() == 2
+    want = int(re.search(r"#define PBN_ABI_VERSION (\d+)", (ROOT / "include" / "pbn_abi.h").read_text()).group(1))
+    assert _lib.lib.pbn_abi_version() == want
 
 
 def test_net_create_validates_on_host():
