@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--rollout", type=int, default=64, help="updates per launch for the supplementary rollout line")
     p.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
+    p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
+    p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
     p.add_argument("--dist-backend", default="nccl",
                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
                         "ranks share one GPU for rehearsals")
@@ -81,6 +83,68 @@ def cpu_baseline(net, seconds: float):
             "sample": f"oracle/pbn_oracle.c orc_step_philox, {net.name}, {B} envs x {T} updates "
                       f"({dt:.1f} s, OpenMP {threads} threads)",
             "reference_python_1core_measured_in_build_container": "20-28k env-steps/s (BASELINE.md)"}
+
+
+def r6_supplement(args, world, rank, device, dist):
+    """BASELINE config 5 beside the main line: the multi-flip until-attractor env
+    (pbn_target_multi.py:119-154) on Bittner-200, ``--r6-batch`` envs per GPU (131,072: 1M
+    over 8 GPUs), T = horizon = 100 env steps per chunk written to a device chunk and
+    all-gathered across ranks (RCCL) while the next chunk runs. Synthetic attractors: the
+    r6_bittner199 fixture's cubes; A = 4 action slots (0 w.p. 0.75); update cap 4,096."""
+    import numpy as np
+    import torch
+
+    from gym_pbn_amd.batch import EnvConfig, Net, PBNBatch, attractors_from_cubes
+    from gym_pbn_amd.network import load_network
+    from gym_pbn_amd.rollout import TrajectoryCollector, gather_chunk
+    from gym_pbn_amd.shard import max_over_ranks, shard_for
+
+    T, B, A = 100, args.r6_batch, 4
+    z = np.load(ROOT / "tests" / "golden" / "r6_bittner199.npz", allow_pickle=False)
+    net = Net(load_network("bittner199"))
+    cfg = EnvConfig(net, attractors_from_cubes(z["cube_care"], z["cube_value"], z["cube_attractor"], net.n_nodes),
+                    horizon=T)
+    sh = shard_for(rank, world, B)
+    dev = torch.device("cuda", device)
+    b = PBNBatch(net, B, device=device, env_id_base=sh.env_base, seed=0xAC7)
+    col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=4096, dist=dist)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xAC7 + rank)
+    v = torch.randint(1, net.n_nodes + 1, (T, B, A), device=dev, generator=g, dtype=torch.int32)
+    acts = (v * (torch.rand((T, B, A), device=dev, generator=g) >= 0.75)).to(torch.int32).contiguous()
+    col.step_chunk(acts)  # warm-up chunk
+    col.finish()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ups = torch.zeros((), dtype=torch.int64, device=dev)
+    t0 = time.perf_counter()
+    for _ in range(args.r6_chunks):
+        buf, _ = col.step_chunk(acts)
+        ups += buf["n_updates"].to(torch.int64).sum()
+    col.finish()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
+    if dist is not None:
+        dist.all_reduce(ups)
+    out = {"metric": "R6 env-steps/s (whole node) incl. per-chunk trajectory all-gather", "unit": "env-steps/s",
+           "value": world * B * T * args.r6_chunks / dt, "node_updates_per_s": float(ups.item()) / dt,
+           "batch_per_gpu": B, "global_batch": world * B, "T": T, "A": A, "update_cap": 4096,
+           "chunks": args.r6_chunks, "s_per_chunk": dt / args.r6_chunks,
+           "chunk_bytes_per_gpu": sum(t.numel() * t.element_size() for t in buf.values())}
+    if dist is not None:  # the gather alone: bytes received per GPU / time
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        gather_chunk(buf, dist)
+        torch.cuda.synchronize()
+        tg = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
+        out["all_gather_GBs_per_gpu"] = out["chunk_bytes_per_gpu"] * (world - 1) / tg / 1e9
+        out["all_gather_s"] = tg
+    b.close()
+    return out
 
 
 def main():
@@ -207,7 +271,7 @@ def main():
                 "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
                 "traffic_source": pmc_src,
                 # measured HBM-side bytes per launch / launch time: the kernel stores only the
-                # 16-B halves that changed and re-reads a 32 MiB state the 256 MB MALL can hold,
+                # envs that changed and re-reads a 32 MiB state the 256 MB MALL can hold,
                 # so the algorithmic rate above can exceed the HBM peak
                 "traffic_GBs": (traffic / avg_kernel_s / 1e9) if (traffic and launches) else None,
                 "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if (traffic and launches) else None,
@@ -215,10 +279,18 @@ def main():
             "node_updates_per_s": value,
             "rollout": rollout,
         }
+    batch.close()
+    r6 = None
+    if args.r6_chunks > 0:
+        try:
+            r6 = r6_supplement(args, world, rank, device, dist)
+        except Exception as exc:  # a supplement must not cost the main line
+            r6 = {"error": f"{type(exc).__name__}: {exc}"}
+    if rank == 0:
+        out["config5_r6"] = r6
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(net, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    batch.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

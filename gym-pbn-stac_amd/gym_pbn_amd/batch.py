@@ -177,6 +177,20 @@ def cube_arrays(cubes: Sequence, n_nodes: int):
     return care, val
 
 
+def attractors_from_cubes(care, value, attractor_of, n_nodes: int):
+    """Rebuild ``all_attractors`` (lists of int / '*' tuples) from packed cube arrays.
+
+    ``care``/``value`` [H][W] uint64 as :func:`cube_arrays` makes them, ``attractor_of`` [H]
+    the attractor index of every cube (the layout of the r6 fixtures).
+    """
+    c = unpack_bits(np.asarray(care, np.uint64), n_nodes)
+    v = unpack_bits(np.asarray(value, np.uint64), n_nodes)
+    out = {}
+    for h, a in enumerate(np.asarray(attractor_of).tolist()):
+        out.setdefault(int(a), []).append(tuple(int(x) if m else "*" for m, x in zip(c[h], v[h])))
+    return [out[k] for k in sorted(out)]
+
+
 class PBNBatch:
     """B independent envs of one network on one GPU."""
 
@@ -340,4 +354,5 @@ class PBNBatch:
         return ms.value, n.value
 
 
-__all__ = ["Net", "EnvConfig", "PBNBatch", "pack_bits", "unpack_bits", "cube_arrays", "KIND_PREDICTOR_MIX"]
+__all__ = ["Net", "EnvConfig", "PBNBatch", "pack_bits", "unpack_bits", "cube_arrays", "attractors_from_cubes",
+           "KIND_PREDICTOR_MIX"]

@@ -40,12 +40,6 @@ def r6_config(z):
 
 def cubes_to_attractors(z, n_nodes):
     """Rebuild all_attractors (lists of '*'/int tuples) from an r6 fixture's care/value arrays."""
-    from gym_pbn_amd.batch import unpack_bits
+    from gym_pbn_amd.batch import attractors_from_cubes
 
-    care = unpack_bits(z["cube_care"], n_nodes)
-    val = unpack_bits(z["cube_value"], n_nodes)
-    out = {}
-    for h, a in enumerate(z["cube_attractor"]):
-        cube = tuple(int(v) if c else "*" for c, v in zip(care[h], val[h]))
-        out.setdefault(int(a), []).append(cube)
-    return [out[k] for k in sorted(out)]
+    return attractors_from_cubes(z["cube_care"], z["cube_value"], z["cube_attractor"], n_nodes)
