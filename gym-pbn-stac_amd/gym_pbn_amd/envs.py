@@ -147,6 +147,78 @@ class PBN:
             self._b.step(1)
 
 
+class VecPBNEnv:
+    """B copies of the ``PBN-v0`` MDP (``pbn_env.py:125-188``) stepped in one launch.
+
+    ``step(actions)`` takes ``[B]`` ints: node ``a`` is flipped when ``a != 0`` (``PBNEnv``
+    flips ``action``, not ``action - 1``, :141-142), then one ``PBN.step`` (R4) per env;
+    reward +20 and terminated when the state is in ``target_nodes`` (expanded by the
+    attractors that meet it, :57-59), else -4 and another -1 for an action; truncated
+    is always False. Rewards are computed on the host from the packed states.
+    ``auto_reset`` resets ended envs to a state drawn uniformly from the attracting set
+    (SB3 VecEnv convention; the reference env never resets itself).
+    """
+
+    def __init__(self, PBN_data=None, logic_func_data=None, goal_config=None, n_envs: int = 1, *,
+                 all_attractors=None, device: int = 0, seed: int = 0, env_id_base: int = 0, auto_reset: bool = False):
+        if PBN_data is not None and len(PBN_data) != 0:
+            net = TruthTableNetwork.from_pbn_data(PBN_data)
+        else:
+            net = TruthTableNetwork.from_logic_funcs(*logic_func_data)
+        self.network = net
+        self.N = net.n_nodes
+        self.num_envs = int(n_envs)
+        if all_attractors is None:
+            from .stg import compute_attractors
+
+            all_attractors = compute_attractors(net)
+        self.all_attractors = [set(tuple(int(v) for v in s) for s in a) for a in all_attractors]
+        target = set(goal_config["target_nodes"])
+        for attractor in self.all_attractors:
+            if target & attractor:
+                target |= attractor
+        self.target_nodes = target
+        self._target_words = np.unique(pack_bits(np.array(sorted(target), np.uint8)), axis=0) if target else None
+        self._attracting = np.array(sorted(set.union(*self.all_attractors)), np.uint8)
+        self.batch = PBNBatch(Net(net), self.num_envs, device=device, env_id_base=env_id_base, seed=seed)
+        self.auto_reset = auto_reset
+        self._rng = np.random.default_rng(seed)
+
+    def _in_target(self, words) -> np.ndarray:
+        if self._target_words is None:
+            return np.zeros(words.shape[0], bool)
+        W = words.shape[1]
+        key = np.ascontiguousarray(words).view(np.dtype((np.void, 8 * W))).ravel()
+        tk = np.ascontiguousarray(self._target_words).view(np.dtype((np.void, 8 * W))).ravel()
+        return np.isin(key, tk)
+
+    def reset(self, mask=None) -> np.ndarray:
+        """States drawn uniformly from the attracting set (node 0 cleared as PBN.reset does)."""
+        m = np.ones(self.num_envs, bool) if mask is None else np.asarray(mask, bool)
+        bits = self.batch.get_bits()
+        pick = self._attracting[self._rng.integers(0, len(self._attracting), size=self.num_envs)]
+        bits[m] = pick[m]
+        bits[:, 0] = 0
+        self.batch.set_bits(bits)
+        return bits
+
+    def step(self, actions):
+        a = np.asarray(actions, dtype=np.int64).reshape(self.num_envs)
+        if (a < 0).any() or (a >= self.N).any():
+            raise Exception("Invalid action, not in action space.")  # pbn_env.py:138-139
+        if (a != 0).any():
+            self.batch.flip((a + 1).astype(np.int32)[:, None] * (a != 0)[:, None], offset=1, dedup=True)
+        self.batch.step(1)
+        words = self.batch.get_state()
+        term = self._in_target(words)
+        reward = np.where(term, 20, -4 - (a != 0).astype(np.int64)).astype(np.int64)
+        trunc = np.zeros(self.num_envs, bool)
+        obs = unpack_bits(words, self.N)
+        if self.auto_reset and term.any():
+            self.reset(term)
+        return obs, reward, term, trunc, {"obs_words": words}
+
+
 class VecPBNTargetMultiEnv:
     """B copies of the multi-flip until-attractor MDP (pbn_target_multi.py:119-259) in one launch.
 
@@ -427,5 +499,5 @@ class PBNEnv:
         return observation, reward, terminated, truncated, {"observation_idx": self._state_to_idx(observation)}
 
 
-__all__ = ["Graph", "PBN", "PBNTargetEnv", "PBNTargetMultiEnv", "VecPBNTargetMultiEnv", "PBNEnv", "state_to_idx",
-           "pack_bits"]
+__all__ = ["Graph", "PBN", "PBNTargetEnv", "PBNTargetMultiEnv", "VecPBNTargetMultiEnv", "VecPBNEnv", "PBNEnv",
+           "state_to_idx", "pack_bits"]

@@ -102,3 +102,37 @@ def test_env_replay_matches_reference(ci):
             assert (bool(term), bool(trunc)) == (st["terminated"], st["truncated"]), where
             assert info.get("interval") == st["interval"], where
             assert info["observation_idx"] == st["observation_idx"], where
+
+
+@pytest.mark.gpu
+def test_vec_pbn_env_matches_single_env_rules():
+    """VecPBNEnv: B envs of PBN-v0 in one launch; rewards/termination as PBNEnv._get_reward
+    (pbn_env.py:156-188) on the same device transitions (a twin batch stepped by hand)."""
+    from gym_pbn_amd.batch import Net, PBNBatch, unpack_bits
+    from gym_pbn_amd.envs import VecPBNEnv
+
+    case = next(c for c in KAT["cases"] if c["network"] == "tt6" and c["kind"] == "PBNEnv")
+    src = _source("tt6")
+    target = {tuple(t) for t in case["target"]}
+    B = 257
+    v = VecPBNEnv(src["PBN_data"], goal_config={"target_nodes": target}, n_envs=B, seed=3)
+    twin = PBNBatch(Net(v.network), B, seed=3)
+    obs = v.reset()
+    twin.set_bits(obs)
+    rng = np.random.default_rng(0)
+    for t in range(20):
+        a = rng.integers(0, v.N, size=B)
+        a[rng.random(B) < 0.5] = 0
+        o, r, term, trunc, info = v.step(a)
+        bits = twin.get_bits()
+        for e in np.nonzero(a)[0]:
+            bits[e, a[e]] ^= 1  # PBNEnv flips node `action` (pbn_env.py:141-142)
+        twin.set_bits(bits)
+        twin.step(1)
+        ref = twin.get_bits()
+        assert np.array_equal(o, ref), t
+        exp_term = np.array([tuple(int(x) for x in row) in v.target_nodes for row in ref])
+        assert np.array_equal(term, exp_term) and not trunc.any()
+        assert np.array_equal(r, np.where(exp_term, 20, -4 - (a != 0)))
+    with pytest.raises(Exception):
+        v.step(np.full(B, v.N))
