@@ -430,31 +430,32 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         bool done = false;
         if constexpr (FAST == 2) {
             const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+            // branch-free per lane: a lane that is done keeps iterating masked (no break, so
+            // no per-lane exit bookkeeping); the wave leaves the chunk when no lane is active
+            bool act = true;
             for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
-                if (used >= a.update_cap) {
-                    capped = true;
-                    done = true;
-                    break;
-                }
-                const uint32_t ent = gbuf[c * 64 + lane];
+                const bool cap_now = used >= a.update_cap;
+                capped |= act && cap_now;
+                act = act && !cap_now;
+                const uint32_t ent = act ? (uint32_t)gbuf[c * 64 + lane] : 0u;
                 const uint32_t i = ent & 0x1FFu;
                 const uint64_t rec = recs[i * a.L.pmax + (ent >> 9)];
                 const uint32_t d = i >> 5, sh = i & 31u;
                 const uint32_t self = P.get(d);
                 const uint32_t y = predictor_apply(P, i, self, rec);
                 const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-                P.put(d, nv);
-                ++used;
+                if (act) P.put(d, nv);
+                used += act ? 1u : 0u;
                 const uint2 nd = ndelta[i];
-                const bool changed = nv != self;
+                const bool changed = act && nv != self;
                 m_lo += changed ? (y ? nd.x : 0u - nd.x) : 0u;
                 m_hi += changed ? (y ? nd.y : 0u - nd.y) : 0u;
-                // :134 the first update is never tested: the check at used == 1 is on o0
-                if ((used == 1 && !a.first_tested) ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u) {
-                    done = true;
-                    break;
-                }
+                const bool hit = act && ((used == 1 && !a.first_tested)
+                                             ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u);
+                act = act && !hit;
+                if (__ballot(act) == 0) break;
             }
+            done = !act;
         } else
         for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
             if (used >= a.update_cap) {
