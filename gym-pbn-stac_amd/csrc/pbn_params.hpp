@@ -162,7 +162,10 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
 int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast);
-constexpr uint32_t ENV_CHUNK = 16;          // updates per lane between refill rounds
+#ifndef PBN_ENV_CHUNK
+#define PBN_ENV_CHUNK 32
+#endif
+constexpr uint32_t ENV_CHUNK = PBN_ENV_CHUNK;  // updates per lane between refill rounds
 constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
