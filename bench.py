@@ -106,32 +106,45 @@ def r6_supplement(args, world, rank, device, dist):
                     horizon=T)
     sh = shard_for(rank, world, B)
     dev = torch.device("cuda", device)
-    b = PBNBatch(net, B, device=device, env_id_base=sh.env_base, seed=0xAC7)
-    col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=4096, dist=dist)
     g = torch.Generator(device=dev)
     g.manual_seed(0xAC7 + rank)
     v = torch.randint(1, net.n_nodes + 1, (T, B, A), device=dev, generator=g, dtype=torch.int32)
     acts = (v * (torch.rand((T, B, A), device=dev, generator=g) >= 0.75)).to(torch.int32).contiguous()
-    col.step_chunk(acts)  # warm-up chunk
-    col.finish()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    ups = torch.zeros((), dtype=torch.int64, device=dev)
-    t0 = time.perf_counter()
-    for _ in range(args.r6_chunks):
-        buf, _ = col.step_chunk(acts)
-        ups += buf["n_updates"].to(torch.int64).sum()
-    col.finish()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
-    if dist is not None:
-        dist.all_reduce(ups)
+
+    def run(fused):
+        b = PBNBatch(net, B, device=device, env_id_base=sh.env_base, seed=0xAC7)
+        col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=4096, dist=dist, fused=fused)
+        col.step_chunk(acts)  # warm-up chunk
+        col.finish()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        ups = torch.zeros((), dtype=torch.int64, device=dev)
+        t0 = time.perf_counter()
+        for _ in range(args.r6_chunks):
+            buf, _ = col.step_chunk(acts)
+            ups += buf["n_updates"].to(torch.int64).sum()
+        col.finish()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        dt = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
+        if dist is not None:
+            dist.all_reduce(ups)
+        lanes = b.info()["env_lanes"]
+        return b, buf, dt, float(ups.item()), lanes
+
+    # closed-loop shape first (one launch per env step, as an agent in the loop needs), then the
+    # open-loop collector (actions known for the chunk: one launch walks each env through T steps)
+    b, buf, dt_step, ups_step, _ = run(False)
+    b.close()
+    b, buf, dt, ups, lanes = run(True)
     out = {"metric": "R6 env-steps/s (whole node) incl. per-chunk trajectory all-gather", "unit": "env-steps/s",
-           "value": world * B * T * args.r6_chunks / dt, "node_updates_per_s": float(ups.item()) / dt,
-           "batch_per_gpu": B, "global_batch": world * B, "T": T, "A": A, "update_cap": 4096,
+           "value": world * B * T * args.r6_chunks / dt, "node_updates_per_s": ups / dt,
+           "launch": "one per chunk (T env steps per env in one launch; actions known for the chunk)",
+           "value_one_launch_per_env_step": world * B * T * args.r6_chunks / dt_step,
+           "node_updates_per_s_one_launch_per_env_step": ups_step / dt_step,
+           "batch_per_gpu": B, "global_batch": world * B, "T": T, "A": A, "update_cap": 4096, "env_lanes": lanes,
            "chunks": args.r6_chunks, "s_per_chunk": dt / args.r6_chunks,
            "chunk_bytes_per_gpu": sum(t.numel() * t.element_size() for t in buf.values())}
     if dist is not None:  # the gather alone: bytes received per GPU / time

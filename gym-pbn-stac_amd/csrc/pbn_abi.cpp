@@ -128,6 +128,7 @@ struct pbn_batch {
     hipStream_t stream = nullptr;
     uint64_t B = 0, env_base = 0, seed = 0, update_count = 0;
     uint32_t env_calls = 0, reset_count = 0;
+    int env_lanes = 0;  // lanes per env of the last R6 launch
     uint64_t* d_state = nullptr;
     int64_t* d_nsteps = nullptr;
     int32_t* d_error = nullptr;
@@ -436,6 +437,7 @@ int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
     info->env_call_count = b->env_calls;
     info->reset_count = b->reset_count;
     info->mt_ready = b->mt_ready;
+    info->env_lanes = b->env_lanes;
     return 0;
 }
 
@@ -894,18 +896,35 @@ int pbn_get_n_steps(pbn_batch* b, int64_t* n_steps) {
     return 0;
 }
 
+// Lanes per env for the R6 kernel: 1 (lane mode, k_env) while the batch fills the chip
+// several times over; group mode where it does not and the until-attractor tail would
+// leave lanes idle (measured: DESIGN.md section 6).
+// Per-step call, Bittner-200, 1 MI355X (256 CUs): G = 8 beats lane mode up to 16k envs (0.21 vs
+// 0.33 ms at B = 1, 0.88 vs 1.99 ms at 8k), ties at 32k, loses at 64k (2.31 vs 2.08 ms).
+static int env_group_size(const pbn_batch* b) {
+    return b->B * 8 <= (uint64_t)b->n_cu * 768 ? 8 : 1;
+}
+
 static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A, int dedup, int offset,
                       uint32_t cap, uint64_t* d_obs, int32_t* d_rew, uint8_t* d_flags, uint32_t* d_nup, int replay,
-                      const void* d_off, const void* d_di, const void* d_dk) {
+                      const void* d_off, const void* d_di, const void* d_dk, uint32_t n_calls = 1) {
     const pbn_envcfg::Dev* dv = cfg->on(b->device);
     if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
     // cooperative draw generation: predictor mix, Philox, record index fits the u16 entry
-    const int mode = (cfg->fast && !replay && b->net->kind == KIND_PREDICTOR_MIX && cfg->L.pmax <= 16 &&
-                      b->net->N <= 512 && !getenv("PBNSIM_ENV_NO_GEN"))
-                         ? 2
-                         : cfg->fast;
+    int mode = (cfg->fast && !replay && b->net->kind == KIND_PREDICTOR_MIX && cfg->L.pmax <= 16 &&
+                b->net->N <= 512 && !getenv("PBNSIM_ENV_NO_GEN"))
+                   ? 2
+                   : cfg->fast;
+    // group mode (k_env_grp: G lanes per env, G updates per round trip)
+    int grp = 1;
+    if (mode == 2 && b->net->N <= 256) {
+        grp = env_group_size(b);
+        if (const char* v = getenv("PBNSIM_ENV_GROUP")) grp = atoi(v);
+        if (grp != 2 && grp != 4 && grp != 8) grp = 1;
+        if (grp > 1) mode = 3;
+    }
     int bpc = 1;
-    if (int e = max_blocks_env(b->W, b->net->kind, mode, cfg->L.bytes, &bpc))
+    if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes, &bpc))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
     if (const char* v = getenv("PBNSIM_ENV_BPC")) bpc = std::max(1, std::min(bpc, atoi(v)));  // tuning knob
     EnvArgs a{};
@@ -923,7 +942,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.off_target = cfg->off_target;
     a.off_ndelta = cfg->off_ndelta;
     a.fast = mode;
-    a.off_gen = cfg->L.bytes + 8u * (uint32_t)b->W * BLOCK;
+    a.grp = grp;
+    a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + 8u * (uint32_t)b->W * BLOCK;
     if (int rc = b->s_counter.ensure(8)) return rc;
     a.counter = (unsigned long long*)b->s_counter.p;
     a.n_cubes = cfg->H;
@@ -939,6 +959,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.reward_success = cfg->reward_success;
     a.action_cost = cfg->action_cost;
     a.first_tested = cfg->first_tested;
+    a.n_calls = n_calls;
     a.draw_off = (const int64_t*)d_off;
     a.draws_i = (const uint32_t*)d_di;
     a.draws_k = (const uint64_t*)d_dk;
@@ -946,10 +967,11 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     HIP_TRY(hipMemsetAsync(b->s_counter.p, 0, 8, b->stream));
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
-    int e = launch_env_multi(b->W, a, replay, b->grid_for(b->B, bpc), b->stream);
+    int e = launch_env_multi(b->W, a, replay, b->grid_for(b->B * (uint64_t)grp, bpc), b->stream);
     if (e) return fail(PBN_E_HIP, "k_env launch: %s", hipGetErrorString((hipError_t)e));
     if (int rc = b->ev_end(stop)) return rc;
-    if (!replay) b->env_calls++;
+    if (!replay) b->env_calls += n_calls;
+    b->env_lanes = grp;
     return 0;
 }
 
@@ -1010,6 +1032,26 @@ int pbn_env_step_multi_device(pbn_batch* b, const pbn_envcfg* cfg_c, const int32
     SET_DEV(b);
     return env_launch(b, cfg, d_actions, A, dedup, offset, update_cap, d_obs, d_reward, d_flags, d_n_updates, 0,
                       nullptr, nullptr, nullptr);
+}
+
+int pbn_env_rollout_multi_device(pbn_batch* b, const pbn_envcfg* cfg_c, uint32_t n_steps, const int32_t* d_actions,
+                                 int A, int dedup, int offset, uint32_t update_cap, uint64_t* d_obs, int32_t* d_reward,
+                                 uint8_t* d_flags, uint32_t* d_n_updates) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(cfg_c, "cfg");
+    CHECK_NN(d_actions, "d_actions");
+    CHECK_NN(d_obs, "d_obs");
+    CHECK_NN(d_reward, "d_reward");
+    CHECK_NN(d_flags, "d_flags");
+    CHECK_NN(d_n_updates, "d_n_updates");
+    pbn_envcfg* cfg = const_cast<pbn_envcfg*>(cfg_c);
+    if (cfg->net != b->net) return fail(PBN_E_INVALID, "envcfg belongs to another network");
+    if (A < 1 || A > 4096) return fail(PBN_E_INVALID, "A=%d outside [1, 4096]", A);
+    if (offset != 0 && offset != 1) return fail(PBN_E_INVALID, "offset must be 0 or 1");
+    if (n_steps < 1 || n_steps > (1u << 20)) return fail(PBN_E_INVALID, "n_steps=%u outside [1, 2^20]", n_steps);
+    SET_DEV(b);
+    return env_launch(b, cfg, d_actions, A, dedup, offset, update_cap, d_obs, d_reward, d_flags, d_n_updates, 0,
+                      nullptr, nullptr, nullptr, n_steps);
 }
 
 int pbn_env_step_multi_replay(pbn_batch* b, const pbn_envcfg* cfg_c, const int32_t* actions, int A, int dedup,

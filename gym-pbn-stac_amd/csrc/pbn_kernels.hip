@@ -322,6 +322,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     const uint32_t lane = __lane_id();
 
     int64_t e = -1;
+    uint32_t t = 0;  // env step of this launch the lane is on (a.n_calls steps per env)
     bool exhausted = false;
     uint64_t o0[W];
     uint32_t m_lo = 0, m_hi = 0;  // FAST: packed per-cube mismatch counters
@@ -330,6 +331,47 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     int64_t nst = 0, dpos = 0, dend = 0;
     int n_act = 0;
     bool capped = false;
+
+    // Start env step t (or the first later step whose action row is valid) of lane env e from
+    // state s: flips (:120-131), observation before the update (:133), plane, counters. With no
+    // step left, write the env's state and step count back and free the lane.
+    auto begin_steps = [&](uint64_t (&s)[W]) {
+        for (; t < a.n_calls; ++t) {
+            uint64_t f[W];
+#pragma unroll
+            for (int k = 0; k < W; ++k) f[k] = s[k];
+            bool bad = false;
+            n_act = apply_actions<W>(f, a.actions + ((uint64_t)t * a.B + (uint64_t)e) * (uint64_t)a.A, a.A,
+                                     a.offset, a.dedup, (int32_t)N, &bad);
+            if (bad) {  // reference raises ValueError; this env step is skipped, the env left untouched
+                atomicOr(a.error, 1);
+                continue;
+            }
+            ++nst;  // :123
+#pragma unroll
+            for (int k = 0; k < W; ++k) o0[k] = f[k];
+            to_plane<W>(P, f);
+            if constexpr (FAST >= 1) {
+                uint32_t m[2] = {0x01010101u, 0x01010101u};  // unused cubes: never zero
+                for (int32_t h = 0; h < H; ++h) {
+                    const uint32_t c = cube_mismatch<W>(f, cubes + (uint64_t)h * 2 * W);
+                    const uint32_t sh = 8u * (uint32_t)(h & 3);
+                    m[h >> 2] = (m[h >> 2] & ~(0xFFu << sh)) | (c << sh);
+                }
+                m_lo = m[0];
+                m_hi = m[1];
+                hit0 = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
+            } else {
+                hit0 = attracting<W>(o0, cubes, H);
+            }
+            used = 0;
+            capped = false;
+            return;
+        }
+        store_state<W>(a.state + (uint64_t)e * W, s);
+        a.n_steps[e] = nst;
+        e = -1;
+    };
 
     for (;;) {
         // ---- refill idle lanes from the global work counter
@@ -347,37 +389,14 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 } else {
                     uint64_t s[W];
                     load_state<W>(a.state + ne * W, s);
-                    bool bad = false;
-                    n_act = apply_actions<W>(s, a.actions + ne * (uint64_t)a.A, a.A, a.offset, a.dedup,
-                                             (int32_t)N, &bad);
-                    if (bad) {  // reference raises ValueError; this env is left untouched
-                        atomicOr(a.error, 1);
-                    } else {
-                        e = (int64_t)ne;
-                        nst = a.n_steps[ne] + 1;  // :123
-#pragma unroll
-                        for (int k = 0; k < W; ++k) o0[k] = s[k];  // :133 observation before the update
-                        to_plane<W>(P, s);
-                        if constexpr (FAST >= 1) {
-                            uint32_t m[2] = {0x01010101u, 0x01010101u};  // unused cubes: never zero
-                            for (int32_t h = 0; h < H; ++h) {
-                                const uint32_t c = cube_mismatch<W>(s, cubes + (uint64_t)h * 2 * W);
-                                const uint32_t sh = 8u * (uint32_t)(h & 3);
-                                m[h >> 2] = (m[h >> 2] & ~(0xFFu << sh)) | (c << sh);
-                            }
-                            m_lo = m[0];
-                            m_hi = m[1];
-                            hit0 = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
-                        } else {
-                            hit0 = attracting<W>(o0, cubes, H);
-                        }
-                        used = 0;
-                        capped = false;
-                        if constexpr (REPLAY) {
-                            dpos = a.draw_off[ne];
-                            dend = a.draw_off[ne + 1];
-                        }
+                    e = (int64_t)ne;
+                    t = 0;
+                    nst = a.n_steps[ne];
+                    if constexpr (REPLAY) {
+                        dpos = a.draw_off[ne];
+                        dend = a.draw_off[ne + 1];
                     }
+                    begin_steps(s);
                 }
             }
         }
@@ -394,11 +413,13 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             uint8_t* lane_of_rank = gw + ENV_CHUNK * 128;                             // [64]
             uint32_t* used_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64);  // [64]
             uint64_t* gid_tab = reinterpret_cast<uint64_t*>(gw + ENV_CHUNK * 128 + 64 + 256);  // [64]
+            uint32_t* call_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64 + 256 + 512);  // [64]
             const uint32_t nact = (uint32_t)__popcll(act);
             if (e >= 0) {
                 lane_of_rank[__popcll(act & ((1ull << lane) - 1ull))] = (uint8_t)lane;
                 used_tab[lane] = used;
                 gid_tab[lane] = a.env_base + (uint64_t)e;
+                call_tab[lane] = a.call_idx + t;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -411,12 +432,12 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 const uint32_t k = k0 + lane;
                 if (k < total) {
                     const uint32_t sl = nact > 1 ? __umulhi(k, magic) : k, r = k - sl * nact;
-                    const uint32_t t = lane_of_rank[r];
+                    const uint32_t q = lane_of_rank[r];
                     uint32_t w[4];
-                    philox_draw(a.seed, used_tab[t] + sl, a.call_idx, gid_tab[t], STREAM_ENV, w);
+                    philox_draw(a.seed, used_tab[q] + sl, call_tab[q], gid_tab[q], STREAM_ENV, w);
                     const uint32_t i = philox_node<KIND>(w[0], N);
                     const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
-                    gbuf[sl * 64 + t] = (uint16_t)(i | (j << 9));
+                    gbuf[sl * 64 + q] = (uint16_t)(i | (j << 9));
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -432,27 +453,41 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
             // branch-free per lane: a lane that is done keeps iterating masked (no break, so
             // no per-lane exit bookkeeping); the wave leaves the chunk when no lane is active
+            // The entries, records and counter deltas do not depend on the state: they are read
+            // one and two updates ahead, so an update's only LDS round trip on the dependent
+            // chain is its state-plane read (every entry of the chunk was generated for this lane).
             bool act = true;
+            uint32_t e1 = gbuf[lane];  // entry of update c + 1 (record and delta loaded)
+            uint64_t r1 = recs[(e1 & 0x1FFu) * a.L.pmax + (e1 >> 9)];
+            uint2 n1 = ndelta[e1 & 0x1FFu];
+            uint32_t e2 = gbuf[64 + lane];  // entry of update c + 2
+            static_assert(ENV_CHUNK >= 2, "prefetch depth");
             for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
+                const uint32_t ent = e1;
+                const uint64_t rec = r1;
+                const uint2 nd = n1;
+                // unconditional (clamped) prefetches: no branch, so no wait before the plane reads
+                e1 = e2;
+                r1 = recs[(e1 & 0x1FFu) * a.L.pmax + (e1 >> 9)];
+                n1 = ndelta[e1 & 0x1FFu];
+                e2 = gbuf[min(c + 2, ENV_CHUNK - 1) * 64 + lane];
                 const bool cap_now = used >= a.update_cap;
                 capped |= act && cap_now;
                 act = act && !cap_now;
-                const uint32_t ent = act ? (uint32_t)gbuf[c * 64 + lane] : 0u;
                 const uint32_t i = ent & 0x1FFu;
-                const uint64_t rec = recs[i * a.L.pmax + (ent >> 9)];
                 const uint32_t d = i >> 5, sh = i & 31u;
                 const uint32_t self = P.get(d);
                 const uint32_t y = predictor_apply(P, i, self, rec);
                 const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-                if (act) P.put(d, nv);
+                P.put(d, act ? nv : self);
                 used += act ? 1u : 0u;
-                const uint2 nd = ndelta[i];
-                const bool changed = act && nv != self;
+                const bool changed = act & (nv != self);
                 m_lo += changed ? (y ? nd.x : 0u - nd.x) : 0u;
                 m_hi += changed ? (y ? nd.y : 0u - nd.y) : 0u;
-                const bool hit = act && ((used == 1 && !a.first_tested)
-                                             ? hit0 : (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u);
-                act = act && !hit;
+                // bitwise, not short-circuit: no exec-mask branch around the test
+                const bool hz = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
+                const bool hit = act & (((used == 1) & !a.first_tested) ? hit0 : hz);
+                act = act & !hit;
                 if (__ballot(act) == 0) break;
             }
             done = !act;
@@ -476,7 +511,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 ++dpos;
             } else {
                 uint32_t w[4];
-                philox_draw(a.seed, used, a.call_idx, g, STREAM_ENV, w);
+                philox_draw(a.seed, used, a.call_idx + t, g, STREAM_ENV, w);
                 i = philox_node<KIND>(w[0], N);
                 k53 = k53_of(w[1], w[2]);
             }
@@ -507,21 +542,323 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         }
         if (!done) continue;
 
-        // ---- finish: outputs of step() (:148-154)
+        // ---- finish: outputs of step() (:148-154) into step t's slot, then the env's next step
         uint64_t s[W];
         from_plane<W>(P, s);
         uint64_t o[W];
 #pragma unroll
         for (int k = 0; k < W; ++k) o[k] = (used <= 1 && !a.first_tested) ? o0[k] : s[k];
-        const uint64_t eu = (uint64_t)e;
-        store_state<W>(a.state + eu * W, s);
-        store_state<W>(a.obs + eu * W, o);
-        a.n_steps[eu] = nst;
+        const uint64_t eo = (uint64_t)t * a.B + (uint64_t)e;
+        store_state<W>(a.obs + eo * W, o);
         const bool term = cube_match<W>(o, target);  // :190-199 (target[0] only)
-        a.reward[eu] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
-        a.flags[eu] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
-        a.n_updates[eu] = used;
+        a.reward[eo] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
+        a.flags[eo] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
+        a.n_updates[eo] = used;
+        ++t;
+        begin_steps(s);
+    }
+}
+
+// ------------------------------------------------------------------ R6, group mode
+// The same env step with G lanes per env: a block of G consecutive updates of one env is
+// evaluated by the G lanes at once (parallel in time), so one env advances G updates per
+// round trip instead of one. The draws of the block do not depend on the state (Philox
+// counter = update index), so lane k knows its node i_k and predictor record up front;
+// what it needs are the values of its 4 input nodes at time k, i.e. the output of the
+// last update j < k in the block that wrote each input, or the block-start value. The
+// writers are found from the byte-packed node list of the group; the outputs y_k are
+// then the fixed point of y_k = tt_k(inputs from writers), a DAG of depth < G: every
+// round that changes nothing is exact. Per-update mismatch deltas are prefix-summed
+// across the group (packed byte counters, as in k_env), the first update whose counters
+// hit a cube ends the env step, and the final writer of each node in the committed
+// prefix sets its bit in the env's LDS row (ds_or / ds_and: distinct nodes, possibly one
+// dword). Same Philox counters as k_env, so the results are bit-identical to lane mode.
+//
+// Used where the batch is small against the chip (BASELINE config 5: 131,072 envs per
+// GPU): there lane mode is latency-bound on the tail of long until-attractor loops.
+// Requirements: predictor mix, N <= 256 (byte-packed node list), fast byte counters.
+
+template <int G>
+__device__ __forceinline__ uint32_t grp_bcast(uint32_t v, uint32_t j) {
+    static_assert(G == 2 || G == 4 || G == 8, "group size");
+    if constexpr (G <= 4) {
+        // quad_perm [j,j,j,j] (G == 2: lanes 0/1 and 2/3 of each quad form two groups)
+        switch (j) {
+            case 0: return G == 2 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false)   // [0,0,2,2]
+                                  : (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);  // [0,0,0,0]
+            case 1: return G == 2 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false)   // [1,1,3,3]
+                                  : (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xF, 0xF, false);  // [1,1,1,1]
+            case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, false);
+            default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, false);
+        }
+    } else {
+        // ds_swizzle bit-mask mode within 32 lanes: src = (lane & 0x18) | j
+        switch (j) {
+            case 0: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (0 << 5));
+            case 1: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (1 << 5));
+            case 2: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (2 << 5));
+            case 3: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (3 << 5));
+            case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (4 << 5));
+            case 5: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (5 << 5));
+            case 6: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (6 << 5));
+            default: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (7 << 5));
+        }
+    }
+}
+
+// value of lane (lane - n) of the same 16-lane row, 0 where that lane is outside the row
+template <int N_>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x110 + N_, 0xF, 0xF, true);
+}
+
+// 0x80 in every byte of v that is zero (exact, no false positives)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+}
+
+// Byte-packed node list of a group (G <= 8: two words). match(x) -> 0x80 per byte j with i_j == x.
+template <int G>
+struct GroupNodes {
+    uint32_t lo = 0, hi = 0;
+    __device__ __forceinline__ explicit GroupNodes(uint32_t i) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t v = grp_bcast<G>(i, (uint32_t)j);
+            if (j < 4)
+                lo |= v << (8 * j);
+            else
+                hi |= v << (8 * (j - 4));
+        }
+        if (G < 4) lo |= 0xFFFFFFFFu << (8 * G);  // unused bytes never match (node < 256)
+        if (G <= 4) hi = 0xFFFFFFFFu;
+    }
+    // bytes j in [j0, j1) of the list equal to x, as a bit mask over j
+    __device__ __forceinline__ uint32_t match(uint32_t x, uint32_t j0, uint32_t j1) const {
+        const uint32_t xx = x * 0x01010101u;
+        const uint32_t zl = zero_bytes(lo ^ xx), zh = zero_bytes(hi ^ xx);
+        // compress 0x80 per byte to one bit per byte
+        uint32_t m = ((zl >> 7) & 1u) | ((zl >> 14) & 2u) | ((zl >> 21) & 4u) | ((zl >> 28) & 8u);
+        if (G > 4) m |= (((zh >> 7) & 1u) | ((zh >> 14) & 2u) | ((zh >> 21) & 4u) | ((zh >> 28) & 8u)) << 4;
+        const uint32_t rng = ((1u << j1) - 1u) & ~((1u << j0) - 1u);
+        return m & rng;
+    }
+};
+
+template <int W, int G>
+__global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    __syncthreads();
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
+    const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
+    const uint2* ndelta = reinterpret_cast<const uint2*>(lds + a.off_ndelta);
+    const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+    const int32_t H = a.n_cubes;
+    const uint32_t lane = __lane_id();
+    const uint32_t k = lane & (G - 1);                     // position in the group = update slot
+    const uint32_t gbase = lane & ~(uint32_t)(G - 1);
+    const uint32_t gmask = (1u << G) - 1u;
+    // the env's 2W dwords, one row per group (bank = group * 2W + dword: 8 groups of W = 4 fill 64 banks)
+    uint32_t* row = reinterpret_cast<uint32_t*>(lds + a.off_gen) + (threadIdx.x / G) * (2 * W);
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+
+    // per-env registers, identical in every lane of the group
+    int64_t e = -1;
+    uint32_t t = 0;  // env step of this launch
+    bool exhausted = false;
+    uint64_t o0[W];
+    uint32_t m_lo = 0, m_hi = 0, used = 0;
+    bool hit0 = false;
+    int64_t nst = 0;
+    int n_act = 0;
+    uint64_t gid = 0;
+
+    // step t (or the first later step with a valid action row) of env e from state s; with no
+    // step left, write the env back and free the group (as begin_steps in k_env)
+    auto begin_steps = [&](uint64_t (&s)[W]) {
+        for (; t < a.n_calls; ++t) {
+            uint64_t f[W];
+#pragma unroll
+            for (int q = 0; q < W; ++q) f[q] = s[q];
+            bool bad = false;
+            n_act = apply_actions<W>(f, a.actions + ((uint64_t)t * a.B + (uint64_t)e) * (uint64_t)a.A, a.A,
+                                     a.offset, a.dedup, (int32_t)N, &bad);
+            if (bad) {  // reference raises ValueError; this env step is skipped, the env left untouched
+                if (k == 0) atomicOr(a.error, 1);
+                continue;
+            }
+            ++nst;  // :123
+#pragma unroll
+            for (int q = 0; q < W; ++q) o0[q] = f[q];  // :133 observation before the update
+            if (k == 0) {
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    row[2 * q] = (uint32_t)f[q];
+                    row[2 * q + 1] = (uint32_t)(f[q] >> 32);
+                }
+            }
+            uint32_t m[2] = {0x01010101u, 0x01010101u};  // unused cubes: never zero
+            for (int32_t h = 0; h < H; ++h) {
+                const uint32_t c = cube_mismatch<W>(f, cubes + (uint64_t)h * 2 * W);
+                const uint32_t sh = 8u * (uint32_t)(h & 3);
+                m[h >> 2] = (m[h >> 2] & ~(0xFFu << sh)) | (c << sh);
+            }
+            m_lo = m[0];
+            m_hi = m[1];
+            hit0 = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
+            used = 0;
+            return;
+        }
+        if (k == 0) {
+            store_state<W>(a.state + (uint64_t)e * W, s);
+            a.n_steps[e] = nst;
+        }
         e = -1;
+    };
+
+    for (;;) {
+        // ---- refill groups without an env: one atomic per wave, ranks over the groups' leaders
+        const bool need = e < 0 && !exhausted;
+        const uint64_t need_lead = __ballot(need && k == 0);
+        if (need_lead) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need_lead) - 1u;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(a.counter, (unsigned long long)__popcll(need_lead));
+            base = __shfl(base, (int)leader);
+            if (need) {
+                const uint64_t ne = base + (uint64_t)__popcll(need_lead & ((1ull << gbase) - 1ull));
+                if (ne >= a.B) {
+                    exhausted = true;
+                } else {
+                    uint64_t s[W];
+                    load_state<W>(a.state + ne * W, s);  // every lane of the group: one request
+                    e = (int64_t)ne;
+                    gid = a.env_base + ne;
+                    t = 0;
+                    nst = a.n_steps[ne];
+                    begin_steps(s);
+                }
+            }
+            wave_sync();
+        }
+        if (__ballot(e >= 0) == 0) {
+            if (__ballot(!exhausted) == 0) break;
+            continue;
+        }
+
+        // ---- one block: update used + k of this group's env in lane k (idle groups compute junk)
+        uint32_t w4[4];
+        philox_draw(a.seed, used + k, a.call_idx + t, gid, STREAM_ENV, w4);
+        const uint32_t i = philox_node<KIND_PREDICTOR_MIX>(w4[0], N);
+        const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, k53_of(w4[1], w4[2]), lds, a.L)];
+        const uint2 nd = ndelta[i];
+        const uint32_t in[4] = {(uint32_t)rec & 0xFFFFu, (uint32_t)(rec >> 16) & 0xFFFFu,
+                                (uint32_t)(rec >> 32) & 0xFFFFu, i};
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (row[in[q] >> 5] >> (in[q] & 31u)) & 1u;  // block-start values
+        const GroupNodes<G> nodes(i);
+        int32_t wr[4];  // last writer j < k of each input, or -1
+        bool dep = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t mm = nodes.match(in[q], 0, k);
+            wr[q] = mm ? 31 - __clz((int)mm) : -1;
+            dep |= mm != 0;
+        }
+        const uint32_t tt = (uint32_t)(rec >> 48);
+        auto eval = [&](uint32_t Y, uint32_t* self_old) {
+            uint32_t x[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = wr[q] >= 0 ? (Y >> wr[q]) & 1u : v[q];
+            *self_old = x[3];
+            return (tt >> ((x[0] << 3) | (x[1] << 2) | (x[2] << 1) | x[3])) & 1u;
+        };
+        uint32_t old;  // node i's value before update k
+        uint32_t y = eval(0u, &old);  // exact where no input has an in-block writer
+        if (__ballot(dep) != 0) {
+            // after round r lanes 0..r are exact, so round G - 1 at the latest changes nothing;
+            // a round that changes nothing has `old` computed from the final outputs
+#pragma unroll 1
+            for (int r = 0; r < G; ++r) {
+                const uint32_t Y = (uint32_t)(__ballot(y != 0u) >> gbase) & gmask;
+                const uint32_t yn = eval(Y, &old);
+                if (__ballot(yn != y) == 0) break;
+                y = yn;
+            }
+        }
+        // mismatch counters after each update of the block (inclusive prefix over the group)
+        const bool changed = y != old;
+        uint32_t dl = changed ? (y ? nd.x : 0u - nd.x) : 0u;
+        uint32_t dh = changed ? (y ? nd.y : 0u - nd.y) : 0u;
+        {
+            uint32_t tl = row_shr<1>(dl), th = row_shr<1>(dh);
+            dl += k >= 1 ? tl : 0u;
+            dh += k >= 1 ? th : 0u;
+            if constexpr (G >= 4) {
+                tl = row_shr<2>(dl);
+                th = row_shr<2>(dh);
+                dl += k >= 2 ? tl : 0u;
+                dh += k >= 2 ? th : 0u;
+            }
+            if constexpr (G >= 8) {
+                tl = row_shr<4>(dl);
+                th = row_shr<4>(dh);
+                dl += k >= 4 ? tl : 0u;
+                dh += k >= 4 ? th : 0u;
+            }
+        }
+        const uint32_t ml = m_lo + dl, mh = m_hi + dh;
+        const bool valid = used + k < a.update_cap;
+        const bool hit = (used + k == 0 && !a.first_tested) ? hit0 : (has_zero_byte(ml) | has_zero_byte(mh)) != 0u;
+        const uint32_t SM = (uint32_t)(__ballot(valid && hit) >> gbase) & gmask;
+        const uint32_t VM = (uint32_t)(__ballot(valid) >> gbase) & gmask;
+        const uint32_t n_done = SM ? (uint32_t)__ffs((int)SM) : (uint32_t)__popc(VM);
+        const bool done = SM != 0u || used + n_done >= a.update_cap;
+        const bool capped = SM == 0u;  // only meaningful when done
+        // commit: the last writer of each node among the first n_done updates sets its bit
+        if (e >= 0 && k < n_done && y != v[3] && nodes.match(i, k + 1, n_done) == 0u) {
+            if (y)
+                atomicOr(&row[i >> 5], 1u << (i & 31u));
+            else
+                atomicAnd(&row[i >> 5], ~(1u << (i & 31u)));
+        }
+        const uint32_t src = gbase + (n_done ? n_done - 1u : 0u);
+        const uint32_t nl = (uint32_t)__shfl((int)ml, (int)src), nh = (uint32_t)__shfl((int)mh, (int)src);
+        if (e >= 0 && n_done) {
+            m_lo = nl;
+            m_hi = nh;
+        }
+        wave_sync();
+        if (e < 0) continue;
+        used += n_done;
+        if (!done) continue;
+
+        // ---- finish: outputs of step() (:148-154) into step t's slot (group leader), next step
+        uint64_t s[W];
+#pragma unroll
+        for (int q = 0; q < W; ++q) s[q] = (uint64_t)row[2 * q] | ((uint64_t)row[2 * q + 1] << 32);
+        if (k == 0) {
+            uint64_t o[W];
+#pragma unroll
+            for (int q = 0; q < W; ++q) o[q] = (used <= 1 && !a.first_tested) ? o0[q] : s[q];
+            const uint64_t eo = (uint64_t)t * a.B + (uint64_t)e;
+            store_state<W>(a.obs + eo * W, o);
+            const bool term = cube_match<W>(o, target);  // :190-199 (target[0] only)
+            a.reward[eo] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
+            a.flags[eo] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
+            a.n_updates[eo] = used;
+        }
+        wave_sync();  // every lane's row reads before the next step rewrites the row
+        ++t;
+        begin_steps(s);
+        wave_sync();
     }
 }
 
@@ -551,8 +888,23 @@ static void* step_fn_w(int W, int store, int replay, int sb) {
     return nullptr;
 }
 
+template <int G>
+static void* env_grp_fn(int W) {
+    switch (W) {
+        case 1: return (void*)k_env_grp<1, G>;
+        case 2: return (void*)k_env_grp<2, G>;
+        case 3: return (void*)k_env_grp<3, G>;
+        case 4: return (void*)k_env_grp<4, G>;
+    }
+    return nullptr;  // N <= 256
+}
+
 template <int KIND>
-static void* env_fn_w(int W, int replay, int fast) {
+static void* env_fn_w(int W, int replay, int fast, int grp) {
+    if (fast == 3) {
+        if (KIND != KIND_PREDICTOR_MIX || replay) return nullptr;
+        return grp == 2 ? env_grp_fn<2>(W) : grp == 4 ? env_grp_fn<4>(W) : grp == 8 ? env_grp_fn<8>(W) : nullptr;
+    }
 #define PBN_ENV_CASE(w)                                                                  \
     case w:                                                                              \
         if (fast == 2 && KIND == KIND_PREDICTOR_MIX && !replay) return (void*)k_env<w, KIND_PREDICTOR_MIX, 0, 2>; \
@@ -642,10 +994,11 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream) {
 }
 
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream) {
-    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast)
-                                              : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast);
+    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast, a.grp)
+                                              : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast, a.grp);
     EnvArgs c = a;
-    return launch(fn, grid, env_lds_bytes(W, a.L.bytes, replay ? std::min(a.fast, 1) : a.fast), stream, &c, sizeof c);
+    return launch(fn, grid, env_lds_bytes(W, a.L.bytes, replay ? std::min(a.fast, 1) : a.fast, a.grp), stream, &c,
+                  sizeof c);
 }
 
 static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
@@ -665,15 +1018,16 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb), blocks_per_cu);
 }
 
-uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast) {
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp) {
+    if (fast == 3) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
     const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
     return fast == 2 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES : planes;
 }
 
-int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu) {
-    void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast)
-                                          : env_fn_w<KIND_PROB_TABLE>(W, 0, fast);
-    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast), blocks_per_cu);
+int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu) {
+    void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast, grp)
+                                          : env_fn_w<KIND_PROB_TABLE>(W, 0, fast, grp);
+    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast, grp), blocks_per_cu);
 }
 
 }  // namespace pbn

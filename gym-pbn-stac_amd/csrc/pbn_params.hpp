@@ -91,7 +91,8 @@ struct EnvArgs {
     int32_t fast;            // 1: <= 8 cubes, each caring about <= 255 nodes (byte counters);
                              // 2: and predictor mix with <= 16 predictors per node, Philox: the
                              //    draws are generated cooperatively by the whole wave
-    uint32_t off_gen;        // fast == 2: per-wave draw buffers (ENV_GEN_WAVE_BYTES each)
+    uint32_t off_gen;        // fast == 2: per-wave draw buffers (ENV_GEN_WAVE_BYTES each);
+                             // fast == 3: per-group env rows (2W dwords per group of grp lanes)
     uint64_t B, env_base, seed;
     uint32_t call_idx, update_cap;
     int32_t A, offset, dedup, horizon, reward_success, action_cost;
@@ -99,6 +100,9 @@ struct EnvArgs {
     const int64_t* draw_off;  // replay mode: [B+1]
     const uint32_t* draws_i;
     const uint64_t* draws_k;
+    int32_t grp;              // fast == 3: lanes per env (2, 4 or 8), k_env_grp
+    uint32_t n_calls;         // env steps per env in this launch: actions [n_calls][B][A], outputs
+                              // [n_calls][B]...; step t draws with Philox c1 = call_idx + t
 };
 
 constexpr uint32_t MT_ROW = 624;
@@ -160,13 +164,13 @@ int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
-int max_blocks_env(int W, int kind, int fast, uint32_t lds_bytes, int* blocks_per_cu);
-uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast);
+int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu);
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp);
 #ifndef PBN_ENV_CHUNK
 #define PBN_ENV_CHUNK 32
 #endif
 constexpr uint32_t ENV_CHUNK = PBN_ENV_CHUNK;  // updates per lane between refill rounds
-constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8;
+constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a);

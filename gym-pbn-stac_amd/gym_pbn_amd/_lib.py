@@ -62,6 +62,7 @@ class BatchInfo(C.Structure):
         ("n_nodes", C.c_int32), ("n_words", C.c_int32), ("kind", C.c_int32), ("device", C.c_int32),
         ("n_envs", C.c_uint64), ("env_id_base", C.c_uint64), ("seed", C.c_uint64), ("update_count", C.c_uint64),
         ("env_call_count", C.c_uint32), ("reset_count", C.c_uint32), ("mt_ready", C.c_int32),
+        ("env_lanes", C.c_int32),
     ]
 
 
@@ -108,6 +109,8 @@ SIGNATURES = {
                                      _u32p]),
     "pbn_env_step_multi_device": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, C.c_uint32, _vp, _vp, _vp,
                                             _vp]),
+    "pbn_env_rollout_multi_device": (C.c_int, [_vp, _vp, C.c_uint32, _vp, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                               _vp, _vp, _vp, _vp]),
     "pbn_env_step_multi_replay": (C.c_int, [_vp, _vp, _i32p, C.c_int, C.c_int, C.c_int, _i64p, _u32p, _u64p, _u64p,
                                             _i32p, _u8p, _u32p]),
     "pbn_ssd_run": (C.c_int, [_vp, _i32p, C.c_int, _u32p, C.c_uint32, _u64p]),

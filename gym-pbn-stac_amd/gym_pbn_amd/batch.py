@@ -327,6 +327,19 @@ class PBNBatch:
                                                 C.c_void_p(d_obs), C.c_void_p(d_reward), C.c_void_p(d_flags),
                                                 C.c_void_p(d_n_updates)))
 
+    def env_rollout_multi_device(self, cfg: EnvConfig, n_steps: int, d_actions: int, A: int, d_obs: int,
+                                 d_reward: int, d_flags: int, d_n_updates: int, offset: int = 1, dedup: bool = True,
+                                 update_cap: int = 1 << 20):
+        """``n_steps`` R6 env steps in one launch (actions known up front, e.g. open-loop or
+        exploration trajectories): device arrays actions ``[n_steps][B][A]`` int32 and outputs
+        ``[n_steps][B][W]`` / ``[n_steps][B]``. Same results as ``n_steps`` calls of
+        :meth:`env_step_multi_device` on the slices; each env walks its steps without waiting
+        for the rest of the batch between them."""
+        L.check(L.lib.pbn_env_rollout_multi_device(self._h, cfg.handle, int(n_steps), C.c_void_p(d_actions), int(A),
+                                                   int(bool(dedup)), int(offset), int(update_cap),
+                                                   C.c_void_p(d_obs), C.c_void_p(d_reward), C.c_void_p(d_flags),
+                                                   C.c_void_p(d_n_updates)))
+
     def synch_step(self, n_steps: int = 1, perturbation_prob: float = 0.0):
         """Synchronous update (base.py:286-303); perturbation_prob > 0 enables perturbations (p=0.001 there)."""
         gap = flip_gap_table(self.n_nodes, perturbation_prob)

@@ -64,12 +64,13 @@ class TrajectoryCollector:
     """T-step R6 chunks on one GPU; optional cross-rank gather of every chunk."""
 
     def __init__(self, batch: PBNBatch, cfg: EnvConfig, T: int, A: int, device, update_cap: int = 1 << 20,
-                 dist=None, offset: int = 1, dedup: bool = True):
+                 dist=None, offset: int = 1, dedup: bool = True, fused: bool = True):
         self.batch, self.cfg = batch, cfg
         self.T, self.A = int(T), int(A)
         self.device = device
         self.update_cap = int(update_cap)
         self.offset, self.dedup = int(offset), bool(dedup)
+        self.fused = bool(fused)  # one launch for the chunk's T steps (else one launch per step)
         self.dist = dist if (dist is not None and dist.is_initialized() and dist.get_world_size() > 1) else None
         B, W = batch.n_envs, batch.n_words
         self.bufs = [alloc_chunk(self.T, B, W, device) for _ in range(2)]
@@ -93,6 +94,10 @@ class TrajectoryCollector:
                           f.stride(0) * f.element_size(), n.stride(0) * n.element_size())
         sa = actions.stride(0) * actions.element_size()
         pa, po, pr, pf, pn = (actions.data_ptr(), o.data_ptr(), r.data_ptr(), f.data_ptr(), n.data_ptr())
+        if self.fused:
+            self.batch.env_rollout_multi_device(self.cfg, T, pa, A, po, pr, pf, pn, offset=self.offset,
+                                                dedup=self.dedup, update_cap=self.update_cap)
+            return
         for t in range(T):
             self.batch.env_step_multi_device(self.cfg, pa + t * sa, A, po + t * so, pr + t * sr, pf + t * sf,
                                              pn + t * sn, offset=self.offset, dedup=self.dedup,

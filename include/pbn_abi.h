@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 2
+#define PBN_ABI_VERSION 4
 
 enum {
     PBN_OK = 0,
@@ -81,6 +81,7 @@ typedef struct {
     uint64_t update_count; /* Philox updates applied so far (batch-wide counter) */
     uint32_t env_call_count, reset_count;
     int32_t mt_ready; /* 1 after pbn_mt_seed */
+    int32_t env_lanes; /* last R6 env-step launch: 1 = one lane per env (k_env), 2/4/8 = lanes per env (k_env_grp) */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).
@@ -168,6 +169,13 @@ int pbn_env_step_multi(pbn_batch *b, const pbn_envcfg *cfg, const int32_t *actio
 int pbn_env_step_multi_device(pbn_batch *b, const pbn_envcfg *cfg, const int32_t *d_actions, int A, int dedup,
                               int offset, uint32_t update_cap, uint64_t *d_obs, int32_t *d_reward, uint8_t *d_flags,
                               uint32_t *d_n_updates);
+/* n_steps consecutive env steps in one launch (open-loop trajectory collection): device arrays
+ * d_actions [n_steps][B][A], outputs [n_steps][B][W] / [n_steps][B]; identical to n_steps calls of
+ * pbn_env_step_multi_device with the actions' slices (same Philox draws, env_call_count += n_steps).
+ * An env step with an out-of-range action is skipped for that env (error flag set, outputs left). */
+int pbn_env_rollout_multi_device(pbn_batch *b, const pbn_envcfg *cfg, uint32_t n_steps, const int32_t *d_actions,
+                                 int A, int dedup, int offset, uint32_t update_cap, uint64_t *d_obs, int32_t *d_reward,
+                                 uint8_t *d_flags, uint32_t *d_n_updates);
 /* Replay mode (parity): draw_offsets [B+1] (int64), draws_i / draws_k the reference's draws, host arrays. */
 int pbn_env_step_multi_replay(pbn_batch *b, const pbn_envcfg *cfg, const int32_t *actions, int A, int dedup,
                               int offset, const int64_t *draw_offsets, const uint32_t *draws_i,

@@ -264,35 +264,96 @@ def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
 
 
 # ----------------------------------------------------------------- config 5: device trajectory chunks
-def test_trajectory_collector_matches_host_api(G):
-    """rollout.TrajectoryCollector writes step t of a chunk into slice t; same results as the host API."""
+@pytest.mark.parametrize("net_name,fused,group", [("bittner28", True, "1"), ("bittner28", False, "1"),
+                                                   ("bittner28", True, "4"), ("bittner199", True, "1"),
+                                                   ("bittner199", True, "8"), ("bittner199", False, "2")])
+def test_trajectory_collector_matches_host_api(G, monkeypatch, net_name, fused, group):
+    """rollout.TrajectoryCollector writes step t of a chunk into slice t; same results as T calls
+    of the host API -- with the chunk as one fused launch (each env walks its T steps alone) or
+    one launch per step, in lane mode and in group mode."""
     import torch
 
     from gym_pbn_amd.rollout import TrajectoryCollector
 
-    z = golden("r6_bittner28.npz")
-    net = G.Net(load_network("bittner28"))
-    cfg = G.EnvConfig(net, cubes_to_attractors(z, 28), horizon=6)
+    monkeypatch.setenv("PBNSIM_ENV_GROUP", group)
+    N = 28 if net_name == "bittner28" else 199
+    z = golden(f"r6_{net_name}.npz")
+    net = G.Net(load_network(net_name))
+    cfg = G.EnvConfig(net, cubes_to_attractors(z, N), horizon=6)
     B, T, A = 3000, 6, 3
     rng = np.random.default_rng(5)
-    acts = rng.integers(0, 29, size=(T, B, A)).astype(np.int32)
+    acts = rng.integers(0, N + 1, size=(T, B, A)).astype(np.int32)
     acts[rng.random(acts.shape) < 0.6] = 0
     dev = torch.device("cuda", 0)
     b1 = G.PBNBatch(net, B, seed=77, env_id_base=123)
-    col = TrajectoryCollector(b1, cfg, T, A, dev, update_cap=1 << 16)
+    col = TrajectoryCollector(b1, cfg, T, A, dev, update_cap=1 << 14, fused=fused)
     buf, gathered = col.step_chunk(torch.from_numpy(acts).to(dev))
     col.finish()
     assert gathered is None
+    assert b1.info()["env_lanes"] == int(group)
     b2 = G.PBNBatch(net, B, seed=77, env_id_base=123)
     b2.env_reset(cfg)
+    monkeypatch.setenv("PBNSIM_ENV_GROUP", "1")
     for t in range(T):
-        obs, rew, flags, nup = b2.env_step_multi(cfg, acts[t], update_cap=1 << 16)
+        obs, rew, flags, nup = b2.env_step_multi(cfg, acts[t], update_cap=1 << 14)
         assert np.array_equal(buf["obs"][t].cpu().numpy().view(np.uint64), obs), t
         assert np.array_equal(buf["reward"][t].cpu().numpy(), rew), t
         assert np.array_equal(buf["flags"][t].cpu().numpy(), flags), t
         assert np.array_equal(buf["n_updates"][t].cpu().numpy().view(np.uint32), nup), t
     assert (flags & 2).all()  # truncated at the horizon == T
     assert np.array_equal(b1.get_state(), b2.get_state())
+    assert np.array_equal(b1.get_n_steps(), b2.get_n_steps())
+    assert b1.info()["env_call_count"] == b2.info()["env_call_count"] == T
+
+
+@pytest.mark.parametrize("group", ["1", "4"])
+def test_env_rollout_skips_invalid_action_steps(G, monkeypatch, group):
+    """An out-of-range action (the reference's flipNode ValueError, base.py:283-284) skips that env
+    step for that env in the fused launch exactly as a per-step device call does: outputs left as
+    they were, state and step count untouched, the error flag raised."""
+    import torch
+
+    from gym_pbn_amd import _lib as L
+
+    monkeypatch.setenv("PBNSIM_ENV_GROUP", group)
+    z = golden("r6_bittner199.npz")
+    net = G.Net(load_network("bittner199"))
+    cfg = G.EnvConfig(net, cubes_to_attractors(z, 199), horizon=100)
+    B, T, A, W = 640, 5, 2, net.n_words
+    rng = np.random.default_rng(9)
+    acts = rng.integers(0, 200, size=(T, B, A)).astype(np.int32)
+    acts[rng.random(acts.shape) < 0.5] = 0
+    acts[2, 7, 1] = 250   # invalid at step 2 for env 7
+    acts[0, 100, 0] = -300  # invalid at step 0 for env 100
+    dev = torch.device("cuda", 0)
+    d_acts = torch.from_numpy(acts).to(dev)
+
+    def out():
+        return (torch.full((T, B, W), -1, dtype=torch.int64, device=dev),
+                torch.full((T, B), -7, dtype=torch.int32, device=dev),
+                torch.full((T, B), 0xEE, dtype=torch.uint8, device=dev),
+                torch.full((T, B), -1, dtype=torch.int32, device=dev))
+
+    res = []
+    for fused in (True, False):
+        b = G.PBNBatch(net, B, seed=3, env_id_base=40)
+        b.env_reset(cfg)
+        o, r, f, n = out()
+        if fused:
+            b.env_rollout_multi_device(cfg, T, d_acts.data_ptr(), A, o.data_ptr(), r.data_ptr(), f.data_ptr(),
+                                       n.data_ptr(), update_cap=4096)
+        else:
+            for t in range(T):
+                b.env_step_multi_device(cfg, d_acts[t].data_ptr(), A, o[t].data_ptr(), r[t].data_ptr(),
+                                        f[t].data_ptr(), n[t].data_ptr(), update_cap=4096)
+        b.sync()
+        res.append((o.cpu().numpy(), r.cpu().numpy(), f.cpu().numpy(), n.cpu().numpy(), b.get_state(),
+                    b.get_n_steps()))
+    for x, y in zip(*res):
+        assert np.array_equal(x, y)
+    o, r, f, n, st, ns = res[0]
+    assert r[2, 7] == -7 and f[0, 100] == 0xEE and (o[0, 100] == -1).all()  # skipped steps left untouched
+    assert ns[7] == T - 1 and ns[100] == T - 1 and ns[0] == T
 
 
 # ----------------------------------------------------------------- env kernel variants vs the oracle
@@ -308,7 +369,8 @@ def _random_cubes(rng, N, H, n_care):
 
 @pytest.mark.parametrize("case", ["b28_gen_cap", "b28_h12_general", "b199_nogen", "tt200_fast", "syn500_gen",
                                   "syn300_wide_cube", "b28_first_tested", "b28_h12_first_tested",
-                                  "tt200_first_tested"])
+                                  "tt200_first_tested", "b199_grp2", "b199_grp4", "b199_grp8", "b28_grp4_cap",
+                                  "b28_grp8_first_tested", "b28_grp2_h8", "b199_grp4_long"])
 def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     """Every k_env variant (cooperative draw generation, byte counters without it, general
     cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs."""
@@ -317,7 +379,11 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     cap, A, B = 3000, 3, 1024
     first = case.endswith("first_tested")  # PBNTargetEnv.step(force=False) semantics
-    if case.startswith("b28"):
+    # k_env_grp (G lanes per env, blocks of G updates resolved in parallel) or lane mode (1)
+    monkeypatch.setenv("PBNSIM_ENV_GROUP", case.split("_grp")[1][0] if "_grp" in case else "1")
+    if case.startswith("b199_grp"):
+        net = load_network("bittner199")
+    elif case.startswith("b28"):
         net = load_network("bittner28")
     elif case == "b199_nogen":
         net = load_network("bittner199")
@@ -328,9 +394,14 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
         n = 500 if case == "syn500_gen" else 300
         net = PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(n, 4, seed=n), name=f"syn{n}")
     N = net.n_nodes
-    if case == "b28_gen_cap":
-        cap = 40
+    if case in ("b28_gen_cap", "b28_grp4_cap"):
+        cap = 41 if "grp" in case else 40  # not a multiple of the group size
         attractors = [_random_cubes(rng, N, 2, 5), _random_cubes(rng, N, 2, 5)]
+    elif case == "b199_grp4_long":  # long until-attractor loops, many capped envs
+        cap = 2001
+        attractors = [_random_cubes(rng, N, 4, 12), _random_cubes(rng, N, 2, 4)]
+    elif case == "b28_grp2_h8":  # 8 cubes: the most the byte counters hold
+        attractors = [_random_cubes(rng, N, 4, 4), _random_cubes(rng, N, 4, 4)]
     elif case.startswith("b28_h12"):
         attractors = [_random_cubes(rng, N, 6, 4), _random_cubes(rng, N, 6, 4)]
     elif case == "syn300_wide_cube":  # one cube caring about 260 > 255 nodes: general matching
@@ -356,6 +427,8 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
         assert np.array_equal(flags, ref["flags"]), case
         st, ns = ref["state"], ref["n_steps"]
         assert np.array_equal(b.get_state(), st), case
-    if case == "b28_gen_cap":
+        if "_grp" in case:
+            assert b.info()["env_lanes"] == int(case.split("_grp")[1][0])  # group mode really ran
+    if case in ("b28_gen_cap", "b28_grp4_cap", "b199_grp4_long"):
         assert (flags & 4).any() and not (flags & 4).all()  # some envs capped, some reached an attractor
     assert (nup > 1).any()

@@ -43,6 +43,7 @@ def main():
     p.add_argument("--chunks", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--cap", type=int, default=4096)
+    p.add_argument("--per-step", action="store_true", help="one launch per env step (closed-loop shape)")
     a = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -60,7 +61,7 @@ def main():
     gnet = Net(net)
     cfg = EnvConfig(gnet, cubes_to_attractors(z, net.n_nodes), horizon=a.T)
     b = PBNBatch(gnet, a.batch, device=local, env_id_base=sh.env_base, seed=0xAC7)
-    col = TrajectoryCollector(b, cfg, a.T, 4, dev, update_cap=a.cap, dist=dist)
+    col = TrajectoryCollector(b, cfg, a.T, 4, dev, update_cap=a.cap, dist=dist, fused=not a.per_step)
     g = torch.Generator(device=dev)
     g.manual_seed(0xAC7 + rank)
 
@@ -100,7 +101,8 @@ def main():
             "value": world * a.batch * a.T * a.chunks / dt, "unit": "env-steps/s", "n_gpus": world,
             "node_updates_per_s": ups / dt, "s_per_chunk": dt / a.chunks,
             "config": {"batch_per_gpu": a.batch, "global_batch": world * a.batch, "T": a.T, "A": 4,
-                       "update_cap": a.cap, "gather": "all_gather_into_tensor per chunk (rccl)" if world > 1
+                       "update_cap": a.cap, "launch": "one per env step" if a.per_step else "one per chunk",
+                       "env_lanes": b.info()["env_lanes"], "gather": "all_gather_into_tensor per chunk (rccl)" if world > 1
                        else "none (1 rank)"},
             "chunk_bytes_per_gpu": chunk_bytes, "gathered_bytes_per_gpu_per_chunk": chunk_bytes * world,
             "last_chunk": {"mean_updates": float(n.mean()), "max_updates": int(n.max()),
