@@ -763,34 +763,48 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
         uint32_t v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = (row[in[q] >> 5] >> (in[q] & 31u)) & 1u;  // block-start values
-        const GroupNodes<G> nodes(i);
-        int32_t wr[4];  // last writer j < k of each input, or -1
-        bool dep = false;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t mm = nodes.match(in[q], 0, k);
-            wr[q] = mm ? 31 - __clz((int)mm) : -1;
-            dep |= mm != 0;
-        }
         const uint32_t tt = (uint32_t)(rec >> 48);
-        auto eval = [&](uint32_t Y, uint32_t* self_old) {
+        auto tt_of = [&](const uint32_t (&x)[4]) { return (tt >> ((x[0] << 3) | (x[1] << 2) | (x[2] << 1) | x[3])) & 1u; };
+        uint32_t y, old;  // node i's new value and its value before update k
+        uint32_t ip = 0;  // G == 2: the partner lane's node
+        GroupNodes<G> nodes(G == 2 ? 0u : i);
+        if constexpr (G == 2) {
+            // pairs: lane 1 depends on lane 0 only where an input is lane 0's node
+            ip = (uint32_t)__builtin_amdgcn_mov_dpp((int)i, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+            const uint32_t y0 = tt_of(v);  // exact in lane 0
+            const uint32_t yb = (uint32_t)__builtin_amdgcn_mov_dpp((int)y0, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
             uint32_t x[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = wr[q] >= 0 ? (Y >> wr[q]) & 1u : v[q];
-            *self_old = x[3];
-            return (tt >> ((x[0] << 3) | (x[1] << 2) | (x[2] << 1) | x[3])) & 1u;
-        };
-        uint32_t old;  // node i's value before update k
-        uint32_t y = eval(0u, &old);  // exact where no input has an in-block writer
-        if (__ballot(dep) != 0) {
-            // after round r lanes 0..r are exact, so round G - 1 at the latest changes nothing;
-            // a round that changes nothing has `old` computed from the final outputs
+            for (int q = 0; q < 4; ++q) x[q] = (k == 1 && in[q] == ip) ? yb : v[q];
+            y = tt_of(x);
+            old = x[3];
+        } else {
+            int32_t wr[4];  // last writer j < k of each input, or -1
+            bool dep = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t mm = nodes.match(in[q], 0, k);
+                wr[q] = mm ? 31 - __clz((int)mm) : -1;
+                dep |= mm != 0;
+            }
+            auto eval = [&](uint32_t Y, uint32_t* self_old) {
+                uint32_t x[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) x[q] = wr[q] >= 0 ? (Y >> wr[q]) & 1u : v[q];
+                *self_old = x[3];
+                return tt_of(x);
+            };
+            y = eval(0u, &old);  // exact where no input has an in-block writer
+            if (__ballot(dep) != 0) {
+                // after round r lanes 0..r are exact, so round G - 1 at the latest changes nothing;
+                // a round that changes nothing has `old` computed from the final outputs
 #pragma unroll 1
-            for (int r = 0; r < G; ++r) {
-                const uint32_t Y = (uint32_t)(__ballot(y != 0u) >> gbase) & gmask;
-                const uint32_t yn = eval(Y, &old);
-                if (__ballot(yn != y) == 0) break;
-                y = yn;
+                for (int r = 0; r < G; ++r) {
+                    const uint32_t Y = (uint32_t)(__ballot(y != 0u) >> gbase) & gmask;
+                    const uint32_t yn = eval(Y, &old);
+                    if (__ballot(yn != y) == 0) break;
+                    y = yn;
+                }
             }
         }
         // mismatch counters after each update of the block (inclusive prefix over the group)
@@ -823,14 +837,26 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
         const bool done = SM != 0u || used + n_done >= a.update_cap;
         const bool capped = SM == 0u;  // only meaningful when done
         // commit: the last writer of each node among the first n_done updates sets its bit
-        if (e >= 0 && k < n_done && y != v[3] && nodes.match(i, k + 1, n_done) == 0u) {
+        const bool last = G == 2 ? (k == 1 || n_done < 2 || ip != i) : nodes.match(i, k + 1, n_done) == 0u;
+        if (e >= 0 && k < n_done && y != v[3] && last) {
             if (y)
                 atomicOr(&row[i >> 5], 1u << (i & 31u));
             else
                 atomicAnd(&row[i >> 5], ~(1u << (i & 31u)));
         }
-        const uint32_t src = gbase + (n_done ? n_done - 1u : 0u);
-        const uint32_t nl = (uint32_t)__shfl((int)ml, (int)src), nh = (uint32_t)__shfl((int)mh, (int)src);
+        uint32_t nl, nh;  // counters after the last committed update
+        if constexpr (G == 2) {
+            const uint32_t l1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)ml, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
+            const uint32_t h1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, 0xF5, 0xF, 0xF, false);
+            const uint32_t l0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)ml, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
+            const uint32_t h0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, 0xA0, 0xF, 0xF, false);
+            nl = n_done == 2 ? l1 : l0;
+            nh = n_done == 2 ? h1 : h0;
+        } else {
+            const uint32_t src = gbase + (n_done ? n_done - 1u : 0u);
+            nl = (uint32_t)__shfl((int)ml, (int)src);
+            nh = (uint32_t)__shfl((int)mh, (int)src);
+        }
         if (e >= 0 && n_done) {
             m_lo = nl;
             m_hi = nh;
