@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
     p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
     p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
+    p.add_argument("--no-config2", dest="config2", action="store_false", help="skip the Bittner-28 supplement")
     p.add_argument("--dist-backend", default="nccl",
                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
                         "ranks share one GPU for rehearsals")
@@ -83,6 +84,36 @@ def cpu_baseline(net, seconds: float):
             "sample": f"oracle/pbn_oracle.c orc_step_philox, {net.name}, {B} envs x {T} updates "
                       f"({dt:.1f} s, OpenMP {threads} threads)",
             "reference_python_1core_measured_in_build_container": "20-28k env-steps/s (BASELINE.md)"}
+
+
+def config2_supplement(device):
+    """BASELINE config 2 beside the main line: Bittner-28 (predictor_sets_28_15_median, N = 28,
+    one state word), 65,536 envs on one GPU (512 KiB of state: launch-bound in step mode), step
+    mode (one Graph.step per env per launch) and rollout (256 updates per launch)."""
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.network import load_network
+
+    B = 65536
+    b = PBNBatch(load_network("bittner28"), B, device=device, seed=0x5EED)
+    b.randomize()
+    b.step(500)
+    b.sync()
+    b.timing(2)
+    n = 2000
+    b.step(n)
+    b.timing(0)
+    ms, launches = b.timing_read()
+    b.rollout(256)
+    b.sync()
+    b.timing(2)
+    for _ in range(5):
+        b.rollout(256)
+    b.timing(0)
+    rms, rl = b.timing_read()
+    b.close()
+    return {"workload": "Bittner-28, 65,536 envs, 1 GPU (BASELINE config 2)",
+            "step_env_steps_per_s": B * n / (ms / 1e3), "step_us_per_launch": ms * 1e3 / max(launches, 1),
+            "rollout_updates_per_launch": 256, "rollout_node_updates_per_s": B * 256 * 5 / (rms / 1e3)}
 
 
 def r6_supplement(args, world, rank, device, dist):
@@ -293,6 +324,12 @@ def main():
             "rollout": rollout,
         }
     batch.close()
+    cfg2 = None
+    if rank == 0 and args.config2:
+        try:
+            cfg2 = config2_supplement(device)
+        except Exception as exc:  # a supplement must not cost the main line
+            cfg2 = {"error": f"{type(exc).__name__}: {exc}"}
     r6 = None
     if args.r6_chunks > 0:
         try:
@@ -300,6 +337,7 @@ def main():
         except Exception as exc:  # a supplement must not cost the main line
             r6 = {"error": f"{type(exc).__name__}: {exc}"}
     if rank == 0:
+        out["config2_bittner28"] = cfg2
         out["config5_r6"] = r6
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(net, args.cpu_seconds)

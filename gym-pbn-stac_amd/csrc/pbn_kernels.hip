@@ -137,6 +137,32 @@ __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
         to_plane<W>(P, cur);
         uint32_t changed = 0;
         const uint64_t g = a.env_base + e;
+        if constexpr (!REPLAY && KIND == KIND_PREDICTOR_MIX) {
+            // software pipeline: the draw and predictor record of update t + 1 (state-independent)
+            // are computed while update t's plane read is in flight -- one env per lane leaves a
+            // wave alone on its SIMD at small batches (65,536 envs: one wave per SIMD)
+            auto draw = [&](uint32_t t, uint32_t* i, uint64_t* rec) {
+                const uint64_t u = a.update_base + t;
+                uint32_t w[4];
+                philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
+                *i = philox_node<KIND>(w[0], N);
+                *rec = predictor_record(*i, k53_of(w[1], w[2]), lds, a.L);
+            };
+            uint32_t i1;
+            uint64_t r1;
+            draw(0, &i1, &r1);
+            for (uint32_t t = 0; t < a.T; ++t) {
+                const uint32_t i = i1;
+                const uint64_t rec = r1;
+                draw(min(t + 1, a.T - 1), &i1, &r1);  // unconditional: no branch before the plane read
+                const uint32_t d = i >> 5, sh = i & 31u;
+                const uint32_t self = P.get(d);
+                const uint32_t y = predictor_apply(P, i, self, rec);
+                const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+                P.put(d, nv);
+                changed |= nv != self;
+            }
+        } else
         for (uint32_t t = 0; t < a.T; ++t) {
             uint32_t i;
             uint64_t k53;
