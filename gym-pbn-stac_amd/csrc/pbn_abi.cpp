@@ -133,7 +133,7 @@ struct pbn_batch {
     int64_t* d_nsteps = nullptr;
     int32_t* d_error = nullptr;
     const void* d_image = nullptr;
-    int n_cu = 0, bpc_step = 1, bpc_env = 1, bpc_base = 1;
+    int n_cu = 0, bpc_step = 1, bpc_env = 1, bpc_base = 1, bpc_roll = 1;
     int step_block = 1024;  // threads per workgroup of the Philox step kernel (256 or 1024)
     int store_mode = STORE_DIRTY;
     int envs_per_thread = 2;  // K: envs each thread walks per launch (pipelined)
@@ -399,6 +399,8 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
     if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, b->step_block, &b->bpc_step)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, BLOCK, &b->bpc_roll, 1)))
+        return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
     if (hipStreamSynchronize(b->stream) != hipSuccess) return bail(fail(PBN_E_HIP, "stream sync"));
     *out = b;
     return 0;
@@ -568,10 +570,16 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
     int store = (T == 1 && !replay) ? b->store_mode : STORE_FULL;
-    const uint64_t K = (uint64_t)b->envs_per_thread;
+    // step mode: K envs per thread (their loads overlap); rollout: one env per lane up to the
+    // resident grid -- its T updates are the work, and more lanes hide more LDS latency
+    // (Bittner-28 @65,536 envs, T = 256: 115 vs 62 G updates/s with K = 2)
+    const bool rollout = T > 1 && !replay;  // k_rollout, 256-thread groups
+    const uint64_t K = rollout ? 1u : (uint64_t)b->envs_per_thread;
     const uint64_t lanes = (b->B + K - 1) / K;
-    const int sb = replay ? BLOCK : b->step_block;
-    const int grid = replay ? b->grid_for(lanes, b->bpc_base) : b->grid_for(lanes, b->bpc_step, sb);
+    const int sb = (replay || rollout) ? BLOCK : b->step_block;
+    const int grid = replay    ? b->grid_for(lanes, b->bpc_base)
+                     : rollout ? b->grid_for(lanes, b->bpc_roll, sb)
+                               : b->grid_for(lanes, b->bpc_step, sb);
     int e = launch_step(b->W, a, store, replay, sb, grid, b->stream);
     if (e) return fail(PBN_E_HIP, "k_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);

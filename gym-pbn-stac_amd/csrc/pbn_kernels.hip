@@ -111,6 +111,10 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
     }
 }
 
+// Step mode (T == 1, Philox; REPLAY == 0) and replay mode (REPLAY == 1: T updates from the
+// caller's draws). Rollout (T > 1, Philox) is its own kernel, k_rollout, so that neither
+// path's code shapes the other's register allocation and schedule (sharing one kernel cost
+// the step path 0.6 us per launch at 1M envs).
 template <int W, int KIND, int STORE, int REPLAY, int SB>
 __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
@@ -120,13 +124,46 @@ __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
     uint64_t cur[W];
     if (e < a.B) load_state<W>(a.state + e * W, cur);
     if constexpr (!REPLAY) {
-        if (a.T == 1) {
-            // Step mode: the draws depend on (seed, update counter, env id) only, so every
-            // draw this thread needs is computed while its state loads are in flight.
-            k_step_single<W, KIND, STORE, SB>(a, lds, e, stride, cur, N);
-            return;
+        // Step mode: the draws depend on (seed, update counter, env id) only, so every
+        // draw this thread needs is computed while its state loads are in flight.
+        k_step_single<W, KIND, STORE, SB>(a, lds, e, stride, cur, N);
+    } else {
+        stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+        __syncthreads();
+        const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+        while (e < a.B) {
+            const uint64_t en = e + stride;
+            uint64_t nxt[W];
+            if (en < a.B) load_state<W>(a.state + en * W, nxt);  // prefetch the next env
+            to_plane<W>(P, cur);
+            for (uint32_t t = 0; t < a.T; ++t) {
+                const uint32_t i = a.replay_node[(uint64_t)t * a.B + e];
+                const uint64_t k53 = a.replay_k53[(uint64_t)t * a.B + e];
+                if constexpr (KIND == KIND_PREDICTOR_MIX)
+                    predictor_update_lds(P, i, k53, lds, a.L);
+                else
+                    table_update_lds(P, i, k53, lds, a.L);
+            }
+            uint64_t out[W];
+            from_plane<W>(P, out);
+            store_state<W>(a.state + e * W, out);
+#pragma unroll
+            for (int k = 0; k < W; ++k) cur[k] = nxt[k];
+            e = en;
         }
     }
+}
+
+// Rollout: T Philox updates per env per launch with the env's state in its LDS plane column;
+// the state is read once and written once (only if it changed).
+template <int W, int KIND, int SB>
+__global__ __launch_bounds__(SB) void k_rollout(StepArgs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const uint64_t stride = (uint64_t)gridDim.x * SB;
+    uint64_t e = (uint64_t)blockIdx.x * SB + threadIdx.x;
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    uint64_t cur[W];
+    if (e < a.B) load_state<W>(a.state + e * W, cur);
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
@@ -137,7 +174,7 @@ __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
         to_plane<W>(P, cur);
         uint32_t changed = 0;
         const uint64_t g = a.env_base + e;
-        if constexpr (!REPLAY && KIND == KIND_PREDICTOR_MIX) {
+        if constexpr (KIND == KIND_PREDICTOR_MIX) {
             // software pipeline: the draw and predictor record of update t + 1 (state-independent)
             // are computed while update t's plane read is in flight -- one env per lane leaves a
             // wave alone on its SIMD at small batches (65,536 envs: one wave per SIMD)
@@ -162,35 +199,20 @@ __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
                 P.put(d, nv);
                 changed |= nv != self;
             }
-        } else
-        for (uint32_t t = 0; t < a.T; ++t) {
-            uint32_t i;
-            uint64_t k53;
-            if constexpr (REPLAY) {
-                i = a.replay_node[(uint64_t)t * a.B + e];
-                k53 = a.replay_k53[(uint64_t)t * a.B + e];
-            } else {
+        } else {
+            for (uint32_t t = 0; t < a.T; ++t) {
                 const uint64_t u = a.update_base + t;
                 uint32_t w[4];
                 philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
-                i = philox_node<KIND>(w[0], N);
-                k53 = k53_of(w[1], w[2]);
+                changed |= table_update_lds(P, philox_node<KIND>(w[0], N), k53_of(w[1], w[2]), lds, a.L);
             }
-            if constexpr (KIND == KIND_PREDICTOR_MIX)
-                changed |= predictor_update_lds(P, i, k53, lds, a.L);
-            else
-                changed |= table_update_lds(P, i, k53, lds, a.L);
         }
         uint64_t out[W];
         from_plane<W>(P, out);
-        if constexpr (STORE == STORE_DIRTY) {
-            bool diff = false;  // whole env, only if it differs (see k_step_single)
+        bool diff = false;  // whole env, only if it differs (see k_step_single)
 #pragma unroll
-            for (int k = 0; k < W; ++k) diff |= out[k] != cur[k];
-            if (changed && diff) store_state<W>(a.state + e * W, out);
-        } else {
-            store_state<W>(a.state + e * W, out);
-        }
+        for (int k = 0; k < W; ++k) diff |= out[k] != cur[k];
+        if (changed && diff) store_state<W>(a.state + e * W, out);
 #pragma unroll
         for (int k = 0; k < W; ++k) cur[k] = nxt[k];
         e = en;
@@ -916,8 +938,9 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
 
 // ------------------------------------------------------------------ dispatch
 template <int W, int KIND>
-static void* step_fn(int store, int replay, int sb) {
+static void* step_fn(int store, int replay, int sb, int rollout) {
     if (replay) return (void*)k_step<W, KIND, STORE_FULL, 1, BLOCK>;
+    if (rollout) return sb == 1024 ? (void*)k_rollout<W, KIND, 1024> : (void*)k_rollout<W, KIND, BLOCK>;
     if (sb == 1024)
         return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0, 1024>
                                     : (void*)k_step<W, KIND, STORE_FULL, 0, 1024>;
@@ -926,16 +949,16 @@ static void* step_fn(int store, int replay, int sb) {
 }
 
 template <int KIND>
-static void* step_fn_w(int W, int store, int replay, int sb) {
+static void* step_fn_w(int W, int store, int replay, int sb, int rollout) {
     switch (W) {
-        case 1: return step_fn<1, KIND>(store, replay, sb);
-        case 2: return step_fn<2, KIND>(store, replay, sb);
-        case 3: return step_fn<3, KIND>(store, replay, sb);
-        case 4: return step_fn<4, KIND>(store, replay, sb);
-        case 5: return step_fn<5, KIND>(store, replay, sb);
-        case 6: return step_fn<6, KIND>(store, replay, sb);
-        case 7: return step_fn<7, KIND>(store, replay, sb);
-        case 8: return step_fn<8, KIND>(store, replay, sb);
+        case 1: return step_fn<1, KIND>(store, replay, sb, rollout);
+        case 2: return step_fn<2, KIND>(store, replay, sb, rollout);
+        case 3: return step_fn<3, KIND>(store, replay, sb, rollout);
+        case 4: return step_fn<4, KIND>(store, replay, sb, rollout);
+        case 5: return step_fn<5, KIND>(store, replay, sb, rollout);
+        case 6: return step_fn<6, KIND>(store, replay, sb, rollout);
+        case 7: return step_fn<7, KIND>(store, replay, sb, rollout);
+        case 8: return step_fn<8, KIND>(store, replay, sb, rollout);
     }
     return nullptr;
 }
@@ -1015,15 +1038,15 @@ uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb) {
     return image_bytes + 8u * (uint32_t)W * (uint32_t)sb;
 }
 
-static void* step_kernel(int W, int kind, int store_mode, int replay, int sb) {
+static void* step_kernel(int W, int kind, int store_mode, int replay, int sb, int rollout) {
     if (replay) sb = BLOCK;
-    return kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay, sb)
-                                      : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay, sb);
+    return kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay, sb, rollout)
+                                      : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay, sb, rollout);
 }
 
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream) {
     if (replay) sb = BLOCK;
-    void* fn = step_kernel(W, a.L.kind, store_mode, replay, sb);
+    void* fn = step_kernel(W, a.L.kind, store_mode, replay, sb, !replay && a.T > 1);
     if (!fn) return (int)hipErrorInvalidValue;
     const uint32_t lds = step_lds_bytes(W, a.L.bytes, sb);
     if (lds > 64u * 1024u) {
@@ -1065,8 +1088,8 @@ static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
     return 0;
 }
 
-int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu) {
-    void* fn = step_kernel(W, kind, STORE_FULL, 0, sb);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout) {
+    void* fn = step_kernel(W, kind, STORE_FULL, 0, sb, rollout);
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb), blocks_per_cu);
 }
 

@@ -163,7 +163,7 @@ uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
-int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout = 0);
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp);
 #ifndef PBN_ENV_CHUNK
