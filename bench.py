@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
     p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
     p.add_argument("--no-config2", dest="config2", action="store_false", help="skip the Bittner-28 supplement")
+    p.add_argument("--no-beyond-mall", dest="beyond_mall", action="store_false",
+                   help="skip the 8M-env (state past the MALL) step-mode supplement")
     p.add_argument("--dist-backend", default="nccl",
                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
                         "ranks share one GPU for rehearsals")
@@ -84,6 +86,30 @@ def cpu_baseline(net, seconds: float):
             "sample": f"oracle/pbn_oracle.c orc_step_philox, {net.name}, {B} envs x {T} updates "
                       f"({dt:.1f} s, OpenMP {threads} threads)",
             "reference_python_1core_measured_in_build_container": "20-28k env-steps/s (BASELINE.md)"}
+
+
+def beyond_mall_supplement(net, device, seed):
+    """Step mode on 8,388,608 envs on ONE GPU (BASELINE config 4's whole batch): 256 MiB of
+    state, past the 256 MB MALL, so every launch streams the state from HBM. Algorithmic bytes
+    / HIP-event kernel time, as for the main line."""
+    from gym_pbn_amd.batch import PBNBatch
+
+    B = 1 << 23
+    b = PBNBatch(net, B, device=device, seed=seed)
+    b.randomize()
+    b.step(20)
+    b.sync()
+    b.timing(2)
+    n = 100
+    b.step(n)
+    b.timing(0)
+    ms, launches = b.timing_read()
+    b.close()
+    s = ms / 1e3 / max(launches, 1)
+    alg = 16 * net.n_words * B
+    return {"workload": "Bittner-200 step mode, 8,388,608 envs on one GPU (state 256 MiB > MALL)",
+            "env_steps_per_s": B / s, "avg_kernel_us": s * 1e6, "alg_bytes_per_launch": alg,
+            "achieved_GBs": alg / s / 1e9, "frac": alg / s / 1e9 / HBM_PEAK_GBS}
 
 
 def config2_supplement(device):
@@ -263,6 +289,13 @@ def main():
                    "node_updates_per_s_per_gpu": B * args.rollout * reps / (rms / 1e3),
                    "kernel_ms": rms / max(rl, 1)}
 
+    beyond = None
+    if rank == 0 and args.beyond_mall and B == 1 << 20:
+        try:
+            beyond = beyond_mall_supplement(net, device, args.seed)
+        except Exception as exc:  # a supplement must not cost the main line
+            beyond = {"error": f"{type(exc).__name__}: {exc}"}
+
     W = net.n_words
     alg_bytes = 16 * W * B  # read + write the packed state of every env
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
@@ -322,6 +355,7 @@ def main():
             },
             "node_updates_per_s": value,
             "rollout": rollout,
+            "beyond_mall_8m": beyond,
         }
     batch.close()
     cfg2 = None
