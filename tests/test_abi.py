@@ -74,3 +74,20 @@ def test_no_silent_cpu_fallback_without_gpu():
     with pytest.raises(_lib.PbnError) as ei:
         PBNBatch("bittner28", 16)
     assert "no HIP device" in str(ei.value) or "HIP" in str(ei.value)
+
+
+def test_batch_create_validates_sizes_on_host():
+    """Empty batches and global env ids past the Philox counter field are refused before any
+    device call (so the same on a CPU-only host and on a GPU box)."""
+    import ctypes as C
+
+    from gym_pbn_amd import _lib
+    from gym_pbn_amd.batch import Net
+    from gym_pbn_amd.network import load_network
+
+    net = Net(load_network("bittner28"))
+    h = C.c_void_p()
+    assert _lib.lib.pbn_batch_create(net.handle, 0, 0, 0, 1, C.byref(h)) == _lib.PBN_E_INVALID
+    assert "n_envs" in _lib.last_error()
+    assert _lib.lib.pbn_batch_create(net.handle, 0, 16, (1 << 56) - 8, 1, C.byref(h)) == _lib.PBN_E_RANGE
+    assert _lib.lib.pbn_batch_create(None, 0, 16, 0, 1, C.byref(h)) == _lib.PBN_E_INVALID

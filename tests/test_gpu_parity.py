@@ -67,6 +67,41 @@ def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
     assert np.array_equal(b.get_state(), o.step_philox(init, 1234, 77, 0, 2 * T))
 
 
+@pytest.mark.parametrize("name", ["bittner199", "bittner28"])
+def test_ragged_batches_and_zero_updates(G, oracle_mod, name):
+    """Batch sizes that fill no wave / workgroup / pair evenly (1, 63, 65, 1023, 1025, 4097, 70001):
+    step, rollout and the R6 env step equal the oracle; zero-update calls change nothing."""
+    net = load_network(name)
+    o = oracle_mod.Oracle(net)
+    rng = np.random.default_rng(3)
+    for B in (1, 63, 65, 1023, 1025, 4097, 70001):
+        b = G.PBNBatch(net, B, seed=99, env_id_base=5)
+        b.randomize()
+        init = b.get_state()
+        b.step(0)
+        b.rollout(0)
+        assert np.array_equal(b.get_state(), init)
+        b.step(3)
+        b.rollout(5)
+        assert np.array_equal(b.get_state(), o.step_philox(init, 99, 5, 0, 8)), B
+        b.close()
+    z = golden(f"r6_{name}.npz")
+    gnet = G.Net(net)
+    cfg = G.EnvConfig(gnet, cubes_to_attractors(z, net.n_nodes), horizon=4)
+    cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care,
+                target_value=cfg.target_value, horizon=4, first_tested=False)
+    for B in (1, 65, 1025):
+        b = G.PBNBatch(gnet, B, seed=8, env_id_base=3)
+        b.env_reset(cfg)
+        st, ns = b.get_state(), np.zeros(B, np.int64)
+        acts = rng.integers(0, net.n_nodes + 1, size=(B, 2)).astype(np.int32)
+        obs, rew, flags, nup = b.env_step_multi(cfg, acts, update_cap=2048)
+        ref = o.env_step_multi(cfgd, st, ns, acts, seed=8, env_base=3, call_idx=0, update_cap=2048)
+        assert np.array_equal(nup, ref["n_updates"]) and np.array_equal(obs, ref["obs"]), B
+        assert np.array_equal(b.get_state(), ref["state"]), B
+        b.close()
+
+
 @pytest.mark.parametrize("store_mode", ["0", "1"])
 def test_store_modes_identical(G, monkeypatch, store_mode):
     monkeypatch.setenv("PBNSIM_STORE_MODE", store_mode)
