@@ -21,6 +21,7 @@ from typing import Optional
 
 import numpy as np
 
+from . import spaces
 from . import _lib as L
 from .batch import EnvConfig, Net, PBNBatch, pack_bits, unpack_bits
 from .network import PredictorNetwork, TruthTableNetwork, load_network
@@ -183,6 +184,9 @@ class VecPBNEnv:
         self.batch = PBNBatch(Net(net), self.num_envs, device=device, env_id_base=env_id_base, seed=seed)
         self.auto_reset = auto_reset
         self._rng = np.random.default_rng(seed)
+        # per-env spaces, as PBNEnv's (pbn_env.py:81-83)
+        self.observation_space = spaces.bool_multibinary(self.N)
+        self.action_space = spaces.Discrete(self.N)
 
     def _in_target(self, words) -> np.ndarray:
         if self._target_words is None:
@@ -240,6 +244,9 @@ class VecPBNTargetMultiEnv:
         self.batch = PBNBatch(net, n_envs, device=device, env_id_base=env_id_base, seed=seed)
         self.update_cap = int(update_cap)
         self.auto_reset = auto_reset
+        # per-env spaces, as PBNTargetMultiEnv's (pbn_target_multi.py:56-59)
+        self.observation_space = spaces.MultiBinary(self.N)
+        self.action_space = spaces.MultiDiscrete(self.N + 1)
 
     def reset(self, mask=None) -> np.ndarray:
         self.batch.env_reset(self.cfg, mask)
@@ -274,6 +281,8 @@ class PBNTargetMultiEnv:
         self.horizon = horizon
         self.target = self.all_attractors[-1]
         self.n_steps = 0
+        self.observation_space = spaces.MultiBinary(self._v.N)  # pbn_target_multi.py:56-59
+        self.action_space = spaces.MultiDiscrete(self._v.N + 1)
 
     @property
     def graph_state(self) -> tuple:
@@ -337,6 +346,8 @@ class PBNTargetEnv:
         self.n_steps = 0
         self.target = None
         self._rng = random.Random()
+        self.observation_space = spaces.MultiBinary(self.N)  # pbn_target.py:90-93
+        self.action_space = spaces.Discrete(self.N + 1)  # intervention nodes + no action
         # force=False runs in the until-attractor kernel, testing the state after every update
         self._cfg = EnvConfig(self.graph._b.net, self.all_attractors, horizon=self.horizon,
                               first_update_tested=True)
@@ -437,6 +448,8 @@ class PBNEnv:
         self.name = name
         self.render_mode = render_mode
         self.step_no = 0
+        self.observation_space = spaces.bool_multibinary(self.PBN.N)  # pbn_env.py:81-83
+        self.action_space = spaces.Discrete(self.PBN.N)
         self._rng = random.Random()
 
     @staticmethod
@@ -489,7 +502,7 @@ class PBNEnv:
         return reward, terminated, False
 
     def step(self, action: int):  # pbn_env.py:125-154
-        if not (0 <= int(action) < self.PBN.N):
+        if not self.action_space.contains(action):
             raise Exception(f"Invalid action {action}, not in action space.")  # :138-139
         if action != 0:
             self.PBN.flip(int(action))  # flips node `action`, not action-1 (:141-142)

@@ -27,6 +27,7 @@ from typing import Sequence, Tuple, Union
 
 import numpy as np
 
+from . import spaces
 from .envs import PBN, PBNEnv
 from .network import TruthTableNetwork
 
@@ -77,11 +78,15 @@ class PBNSampledDataEnv(PBNEnv):
                          **kw)
         self.gamma = gamma
         self.T = T if T is not None else 2 ** self.PBN.N
+        self.primitive_action_space = spaces.Discrete(self.PBN.N + 1)  # sampled_data.py:43-49
+        self.interval_space = spaces.Discrete(self.T, start=1)
+        self.action_space = spaces.Tuple((self.primitive_action_space, self.interval_space))
+        self.discrete_action_space = spaces.Discrete(self.primitive_action_space.n * self.interval_space.n)
 
     def step(self, action: Tuple[int, int]):
-        control_action, interval = action
-        if not (0 <= control_action <= self.PBN.N and 1 <= interval <= self.T):
+        if not self.action_space.contains(action):  # :52-53
             raise Exception(f"Invalid action {action}, not in action space.")
+        control_action, interval = action
         total_reward = 0
         for i in range(interval):
             if control_action != 0:
@@ -104,12 +109,16 @@ class PBNSelfTriggeringEnv(PBNEnv):
                          **kw)
         self.gamma = gamma
         self.T = T
+        self.primitive_action_space = spaces.Discrete(self.PBN.N + 1)  # self_triggering.py:44-49
+        self.prob_space = spaces.Discrete(10, start=1)  # {0.1, ..., 1.0}
+        self.action_space = spaces.Tuple((self.primitive_action_space, self.prob_space))
+        self.discrete_action_space = spaces.Discrete(self.primitive_action_space.n * self.prob_space.n)
         self.successful_reward, self.wrong_attractor_cost, self.action_cost = 1, 0, 1  # :51-54
 
     def step(self, action: Tuple[int, int]):
-        control_action, prob = action
-        if not (0 <= control_action <= self.PBN.N and 1 <= prob <= 10):
+        if not self.action_space.contains(action):  # :56-57
             raise Exception(f"Invalid action {action}, not in action space.")
+        control_action, prob = action
         prob /= 10
         total_reward, i, end = 0, 0, False
         while not end:
@@ -135,6 +144,9 @@ class PBCNEnv(PBNEnv):
                          **kw)
         self.PBN = PBCN(PBN_data, logic_func_data, device=kw.get("device", 0), seed=kw.get("seed", 0))
         self.target_nodes = goal_config["target_nodes"]  # pbcn_env.py:43 (unexpanded)
+        self.observation_space = spaces.bool_multibinary(self.PBN.N)  # pbcn_env.py:41-45
+        self.action_space = spaces.bool_multibinary(self.PBN.M)
+        self.discrete_action_space = spaces.Discrete(2 ** self.PBN.M)
 
     @property
     def M(self) -> int:
@@ -172,6 +184,10 @@ class PBCNSampledDataEnv(PBCNEnv):
                          **kw)
         self.gamma = gamma
         self.T = T if T is not None else 2 ** self.PBN.N
+        self.primitive_action_space = spaces.bool_multibinary(self.M)  # sampled_data.py:118-129
+        self.interval_space = spaces.Discrete(self.T, start=1)
+        self.action_space = spaces.Tuple((self.primitive_action_space, self.interval_space))
+        self.discrete_action_space = spaces.Discrete((2 ** self.M) * self.interval_space.n)
 
     def _idx_to_macro_action(self, i: int):
         action = booleanize(i % (2 ** self.M), self.M).tolist()
@@ -182,12 +198,12 @@ class PBCNSampledDataEnv(PBCNEnv):
             raise Exception("You need to provide a macro action with either `macro_action` or "
                             "`macro_action_discrete`.")
         if _discrete(action):
-            if not (0 <= int(action) < (2 ** self.M) * self.T):
+            if not self.discrete_action_space.contains(action):  # :145-147
                 raise Exception(f"Invalid action {action}, not in action space.")
             action = self._idx_to_macro_action(int(action))
-        control_action, interval = action
-        if len(control_action) != self.M or not (1 <= interval <= self.T):
+        if not self.action_space.contains(action):  # :151-152
             raise Exception(f"Invalid action {action}, not in action space.")
+        control_action, interval = action
         time_step_cost = 1
         total_reward, terminated_step = 0, None
         for i in range(interval):
@@ -215,6 +231,10 @@ class PBCNSelfTriggeringEnv(PBCNEnv):
                          **kw)
         self.gamma = gamma
         self.T = T
+        self.primitive_action_space = spaces.bool_multibinary(self.M)  # self_triggering.py:122-130
+        self.prob_space = spaces.Discrete(10, start=1)
+        self.action_space = spaces.Tuple((self.primitive_action_space, self.prob_space))
+        self.discrete_action_space = spaces.Discrete((2 ** self.M) * self.prob_space.n)
         self.successful_reward, self.wrong_attractor_cost, self.action_cost = 1, 1, 1  # :135-138
 
     def _idx_to_macro_action(self, i: int):
@@ -225,14 +245,14 @@ class PBCNSelfTriggeringEnv(PBCNEnv):
             raise Exception("You need to provide a macro action with either `macro_action` or "
                             "`macro_action_discrete`.")
         if _discrete(action):
-            if not (0 <= int(action) < (2 ** self.M) * 10):
+            if not self.discrete_action_space.contains(action):  # :150-152
                 raise Exception(f"Invalid action {action}, not in action space.")
             action = self._idx_to_macro_action(int(action))
         if type(action[1]) is float:  # self_triggering.py:155-156
             action = (action[0], int(action[1] * 10))
-        control_action, prob = action
-        if len(control_action) != self.M or not (1 <= prob <= 10):
+        if not self.action_space.contains(action):  # :158-159
             raise Exception(f"Invalid action {action}, not in action space.")
+        control_action, prob = action
         prob /= 10
         total_reward, i, end = 0, 0, False
         while not end:

@@ -136,3 +136,44 @@ def test_vec_pbn_env_matches_single_env_rules():
         assert np.array_equal(r, np.where(exp_term, 20, -4 - (a != 0)))
     with pytest.raises(Exception):
         v.step(np.full(B, v.N))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci", range(len(KAT["cases"])),
+                         ids=[f'{c["network"]}-{c["kind"]}' for c in KAT["cases"]])
+def test_env_spaces_match_reference_constructors(ci):
+    """observation / action / discrete-action spaces as the reference constructors build them
+    (pbn_env.py:81-83, pbcn_env.py:41-45, sampled_data.py:43-49,118-129,
+    self_triggering.py:44-48,122-127), and invalid actions rejected through them."""
+    case = KAT["cases"][ci]
+    env = _env(case)
+    kind, N = case["kind"], env.PBN.N
+    assert env.observation_space.shape == (N,)
+    if kind == "PBNEnv":
+        assert env.action_space.n == N and env.action_space.start == 0
+        with pytest.raises(Exception, match="not in action space"):
+            env.step(N)
+        with pytest.raises(Exception, match="not in action space"):
+            env.step(1.0)  # Discrete.contains rejects floats
+    elif kind in ("PBNSampledDataEnv", "PBNSelfTriggeringEnv"):
+        second = env.interval_space if kind == "PBNSampledDataEnv" else env.prob_space
+        assert env.primitive_action_space.n == N + 1 and second.start == 1
+        assert second.n == (env.T if kind == "PBNSampledDataEnv" else 10)
+        assert env.discrete_action_space.n == (N + 1) * second.n
+        assert env.action_space.contains((N, int(second.start)))
+        with pytest.raises(Exception, match="not in action space"):
+            env.step((N + 1, 1))
+        with pytest.raises(Exception, match="not in action space"):
+            env.step((0, 0))
+    else:
+        M = env.M
+        if kind == "PBCNEnv":
+            assert env.action_space.n == M and env.discrete_action_space.n == 2 ** M
+        else:
+            second = env.interval_space if kind == "PBCNSampledDataEnv" else env.prob_space
+            assert env.primitive_action_space.n == M and second.start == 1
+            assert env.discrete_action_space.n == (2 ** M) * second.n
+            with pytest.raises(Exception, match="not in action space"):
+                env.step(env.discrete_action_space.n)
+            with pytest.raises(Exception, match="not in action space"):
+                env.step(([0] * (M + 1), 1))
