@@ -38,19 +38,70 @@ def ssd_counts(network, target_nodes: Sequence[int], iters: int, resets: int, bi
     return b.ssd_counts(target_nodes, iters, bit_flip_prob)
 
 
+def _predict(model, obs: np.ndarray) -> np.ndarray:
+    """``model.predict(state, target, deterministic=True)`` as ``_ssd_run`` calls it (eval.py:97-100:
+    ``target`` is the state again), on the whole batch; a returned tuple is (actions, ...)."""
+    out = model.predict(obs, obs, deterministic=True)
+    if type(out) is tuple:
+        out = out[0]
+    return np.asarray(out).reshape(obs.shape[0], -1)
+
+
+def ssd_counts_controlled(network, target_nodes: Sequence[int], iters: int, resets: int, model, seed: int = 0,
+                          device: int = 0, initial_states: Optional[np.ndarray] = None) -> np.ndarray:
+    """Raw counts [2^g] of the model-controlled run (``_ssd_run`` with a model, eval.py:80-101):
+    per iteration count the bucket, ask the model for an action on every env at once (a
+    batched ``predict``, one call for the ``resets`` envs), flip node ``action - 1`` (0 = none,
+    ``pbn_target.py:266-267``), one async transition (R1/R4, Philox, no bit-flip noise)."""
+    b = PBNBatch(network, resets, device=device, seed=seed)
+    if initial_states is None:
+        b.randomize()
+    else:
+        b.set_state(initial_states)
+    t = np.asarray(target_nodes, dtype=np.int64)
+    weights = (1 << np.arange(t.size - 1, -1, -1)).astype(np.int64)  # first target = MSB
+    counts = np.zeros(1 << t.size, dtype=np.uint64)
+    for _ in range(iters):
+        obs = b.get_bits()
+        np.add.at(counts, obs[:, t].astype(np.int64) @ weights, 1)
+        b.flip(_predict(model, obs).astype(np.int32), offset=1, dedup=True)
+        b.step(1)
+    b.close()
+    return counts
+
+
 def compute_ssd_hist(network, target_nodes: Sequence[int], iters: int = 1_200_000, resets: int = 300,
                      bit_flip_prob: float = 0.01, seed: int = 0, device: int = 0,
-                     initial_states: Optional[np.ndarray] = None):
-    """Normalised SSD histogram as a DataFrame indexed by the bucket bit strings (eval.py:62-69)."""
+                     initial_states: Optional[np.ndarray] = None, model=None):
+    """Normalised SSD histogram as a DataFrame indexed by the bucket bit strings (eval.py:62-69).
+
+    ``model`` given: the controlled SSD (actions from ``model.predict``, no bit-flip noise,
+    eval.py:96-101); otherwise the uncontrolled run with Bernoulli bit flips, all on the device."""
     assert 0 <= bit_flip_prob <= 1, "Invalid Bit Flip Probability value."  # eval.py:32-34
     assert resets > 0, "Invalid resets value."
     assert iters > 0, "Invalid iterations value."
     assert iters // resets, "Resets does not divide the iterations."
     per = iters // resets
-    counts = ssd_counts(network, target_nodes, per, resets, bit_flip_prob, seed, device, initial_states)
+    if model is None:
+        counts = ssd_counts(network, target_nodes, per, resets, bit_flip_prob, seed, device, initial_states)
+    else:
+        counts = ssd_counts_controlled(network, target_nodes, per, resets, model, seed, device, initial_states)
     ssd = counts.astype(np.float64) / resets / per  # mean over resets, then / (iters // resets)
     g = len(target_nodes)
     states = list(map(_bit_seq_to_str, itertools.product([0, 1], repeat=g)))
     import pandas as pd
 
     return pd.DataFrame(list(ssd), index=states, columns=["Value"])
+
+
+def eval_increase(network, target_nodes: Sequence[int], model, target_node_values, original_ssd=None,
+                  iters: int = 1_200_000, resets: int = 300, bit_flip_prob: float = 0.01, seed: int = 0,
+                  device: int = 0) -> float:
+    """Total increase of the favourable buckets between the uncontrolled and the controlled
+    SSD (``eval_increase``, eval.py:106-136). ``target_node_values`` are the favourable
+    target-node value tuples (the reference's ``env.target_node_values``)."""
+    if original_ssd is None:  # cache, as the reference
+        original_ssd = compute_ssd_hist(network, target_nodes, iters, resets, bit_flip_prob, seed, device)
+    model_ssd = compute_ssd_hist(network, target_nodes, iters, resets, bit_flip_prob, seed, device, model=model)
+    states_of_interest = [_bit_seq_to_str(s) for s in target_node_values]
+    return float((model_ssd - original_ssd).loc[states_of_interest, "Value"].sum())

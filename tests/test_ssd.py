@@ -71,3 +71,45 @@ def test_compute_ssd_hist_normalised():
     df = compute_ssd_hist("bittner28", [0, 1, 2, 3, 6, 7, 9], iters=120_000, resets=300, seed=3)
     assert list(df.index[:2]) == ["0000000", "0000001"] and len(df) == 128
     assert abs(df["Value"].sum() - 1.0) < 1e-9
+
+
+class _RulePolicy:
+    """A deterministic stand-in agent: flip node 3 (action 4) when node 0 is set, else nothing;
+    returns (actions, None) like a Stable-Baselines model."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def predict(self, obs, target, deterministic=True):
+        assert deterministic and obs.shape == target.shape
+        self.calls += 1
+        return np.where(obs[:, 0] == 1, 4, 0), None
+
+
+@pytest.mark.gpu
+def test_controlled_ssd_matches_stepwise_oracle(oracle_mod):
+    """Model-in-the-loop SSD (eval.py:96-101): bucket, batched predict, flip action-1, one R1
+    update -- replayed with the oracle's Philox step and numpy flips."""
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.eval import compute_ssd_hist, eval_increase, ssd_counts_controlled
+
+    net = load_network("bittner28")
+    targets, B, iters = [0, 1, 2, 3, 6, 7, 9], 64, 40
+    b = PBNBatch(net, B, seed=11)
+    b.randomize()
+    s0 = b.get_state()
+    pol = _RulePolicy()
+    got = ssd_counts_controlled(net, targets, iters, B, pol, seed=11, initial_states=s0)
+    assert pol.calls == iters
+    o = oracle_mod.Oracle(net)
+    st, want = s0.copy(), np.zeros(1 << len(targets), np.uint64)
+    for u in range(iters):
+        bits = ((st[:, :1] >> np.arange(28, dtype=np.uint64)) & np.uint64(1)).astype(np.int64)
+        np.add.at(want, bits[:, targets] @ (1 << np.arange(len(targets) - 1, -1, -1)), 1)
+        st[bits[:, 0] == 1, 0] ^= np.uint64(1 << 3)  # action 4 flips node 3
+        st = o.step_philox(st, 11, 0, u, 1)
+    assert np.array_equal(got, want)
+    df = compute_ssd_hist(net, targets, iters=iters * B, resets=B, seed=11, model=_RulePolicy())
+    assert abs(df["Value"].sum() - 1.0) < 1e-9
+    inc = eval_increase(net, targets, _RulePolicy(), [(0,) * 7, (1,) * 7], iters=iters * B, resets=B, seed=11)
+    assert np.isfinite(inc)
