@@ -907,10 +907,11 @@ int pbn_get_n_steps(pbn_batch* b, int64_t* n_steps) {
 // Lanes per env for the R6 kernel: 1 (lane mode, k_env) while the batch fills the chip
 // several times over; group mode where it does not and the until-attractor tail would
 // leave lanes idle (measured: DESIGN.md section 6).
-// Per-step call, Bittner-200, 1 MI355X (256 CUs): G = 8 beats lane mode up to 16k envs (0.21 vs
-// 0.33 ms at B = 1, 0.88 vs 1.99 ms at 8k), ties at 32k, loses at 64k (2.31 vs 2.08 ms).
+// Per-step call, Bittner-200, 1 MI355X (256 CUs): G = 8 beats lane mode up to 32k envs (0.21 vs
+// 0.33 ms at B = 1, 0.88 vs 1.99 ms at 8k, 1.85 vs 2.04 ms at 32k) and loses from 64k on (2.31 vs
+// 2.07 ms; 131k: 3.28 vs 2.60 ms) -- the crossover sits near 48k envs.
 static int env_group_size(const pbn_batch* b) {
-    return b->B * 8 <= (uint64_t)b->n_cu * 768 ? 8 : 1;
+    return b->B * 8 <= (uint64_t)b->n_cu * 1536 ? 8 : 1;
 }
 
 static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A, int dedup, int offset,
