@@ -53,9 +53,15 @@ def test_single_env_b1_plumbing(G):
 
 # ----------------------------------------------------------------- Philox mode vs oracle
 @pytest.mark.parametrize("name,B,T", [("bittner28", 4096, 64), ("bittner199", 8192, 40), ("tt200", 4096, 40),
-                                      ("bittner70", 3000, 33), ("tt8", 1000, 50)])
+                                      ("bittner70", 3000, 33), ("tt8", 1000, 50), ("syn500", 2048, 24)])
 def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
-    net = load_network(name)
+    if name == "syn500":  # W = 8 state words: the largest network the build takes (N <= 512)
+        from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
+
+        net = PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(500, 4, seed=500), name="syn500")
+        assert net.n_words == 8
+    else:
+        net = load_network(name)
     o = oracle_mod.Oracle(net)
     b = G.PBNBatch(net, B, seed=1234, env_id_base=77)
     b.randomize()
@@ -138,6 +144,25 @@ def test_full_size_shard_invariance_and_sampled_oracle(G, oracle_mod):
     for e in idx[:50]:
         assert np.array_equal(o.step_philox(init[e:e + 1], 2024, int(e), 0, T)[0], got[e])
     # bits beyond node 198 stay clear
+    assert not (got[:, 3] >> np.uint64(199 - 192)).any()
+
+
+def test_max_batch_single_gpu_sampled_oracle(G, oracle_mod):
+    """BASELINE config 4's whole batch (8,388,608 envs, 256 MiB of state) on one GPU: step and
+    rollout equal the oracle on sampled envs across the id range, bits past node 198 stay clear."""
+    B, T = 1 << 23, 4
+    net = load_network("bittner199")
+    b = G.PBNBatch(net, B, seed=808)
+    b.randomize()
+    init = b.get_state()
+    b.step(T)
+    b.rollout(T)
+    got = b.get_state()
+    b.close()
+    idx = np.concatenate([[0, 1, B // 2, B - 2, B - 1], np.random.default_rng(1).choice(B, 95, replace=False)])
+    o = oracle_mod.Oracle(net)
+    for e in idx:
+        assert np.array_equal(o.step_philox(init[e:e + 1], 808, int(e), 0, 2 * T)[0], got[e]), e
     assert not (got[:, 3] >> np.uint64(199 - 192)).any()
 
 
