@@ -49,8 +49,9 @@ def parse():
     p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
     p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
     p.add_argument("--no-config2", dest="config2", action="store_false", help="skip the Bittner-28 supplement")
-    p.add_argument("--no-beyond-mall", dest="beyond_mall", action="store_false",
-                   help="skip the 8M-env (state past the MALL) step-mode supplement")
+    p.add_argument("--beyond-mall", action="store_true",
+                   help="add the 8M-env (state past the MALL) step-mode supplement (off by default: it launches "
+                        "the bench kernel at another size, which would mix into a rocprof average of the line)")
     p.add_argument("--dist-backend", default="nccl",
                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
                         "ranks share one GPU for rehearsals")

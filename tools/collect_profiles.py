@@ -22,9 +22,9 @@ rows = [r for r in csv.DictReader(open(G / "prof_bench" / "bench_kernel_trace.cs
         if "k_step<4, 1, 1, 0, 1024>" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-w = bench["warmup"]
+w, n = bench["warmup"], bench["steps"]
 check = {"kernel": "pbn::k_step<4, 1, 1, 0, 1024>", "launches": len(d), "warmup_excluded": w,
-         "rocprof_avg_us_timed": sum(d[w:]) / len(d[w:]) / 1e3, "rocprof_avg_us_all": sum(d) / len(d) / 1e3,
+         "rocprof_avg_us_timed": sum(d[w:w + n]) / len(d[w:w + n]) / 1e3, "rocprof_avg_us_all": sum(d) / len(d) / 1e3,
          "bench_hip_event_avg_us": bench["roofline"]["avg_kernel_us"],
          "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (same defaults as the bench line)"}
 (P / f"{tag}_bench_trace_check.json").write_text(json.dumps(check, indent=1) + "\n")
@@ -34,6 +34,10 @@ for k in ("fetch", "write"):
     if src.exists():
         shutil.copy(src, P / f"{tag}_pmc_{k}_size.csv")
 shutil.copy(G / "prof_env" / "env_kernel_stats.csv", P / f"{tag}_env_kernel_stats.csv")
+bm = G / "beyond_mall.json"
+if bm.exists():
+    ls = [l for l in bm.read_text().splitlines() if l.startswith("{")]
+    (P / f"{tag}_beyond_mall_8m.json").write_text(json.dumps(json.loads(ls[-1])["beyond_mall_8m"], indent=1) + "\n")
 for n in ("r6_131k", "r6_1m"):
     ls = [l for l in (G / f"{n}.json").read_text().splitlines() if l.startswith("{")]
     (P / f"{tag}_config5_{n[3:]}.json").write_text(ls[-1] + "\n")
