@@ -125,7 +125,8 @@ struct pbn_envcfg {
 struct pbn_batch {
     pbn_net* net = nullptr;
     int device = 0, W = 0, N = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // the stream every call of this batch runs on
+    hipStream_t own_stream = nullptr;  // created with the batch; `stream` unless pbn_batch_set_stream
     uint64_t B = 0, env_base = 0, seed = 0, update_count = 0;
     uint32_t env_calls = 0, reset_count = 0;
     int env_lanes = 0;  // lanes per env of the last R6 launch
@@ -386,6 +387,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
         b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(PBN_E_HIP, "hipStreamCreate"));
+    b->own_stream = b->stream;
     size_t sb = 8 * (size_t)b->W * n_envs;
     if (hipMalloc(&b->d_state, sb) != hipSuccess) return bail(fail(PBN_E_NOMEM, "state alloc (%zu B)", sb));
     if (hipMalloc(&b->d_nsteps, 8 * n_envs) != hipSuccess) return bail(fail(PBN_E_NOMEM, "n_steps alloc"));
@@ -421,8 +423,21 @@ void pbn_batch_destroy(pbn_batch* b) {
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
                       &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab})
         d->release();
-    if (b->stream) (void)hipStreamDestroy(b->stream);
+    if (b->own_stream) {
+        (void)hipStreamSynchronize(b->stream);
+        (void)hipStreamDestroy(b->own_stream);
+    }
     delete b;
+}
+
+int pbn_batch_set_stream(pbn_batch* b, int own, void* stream) {
+    CHECK_NN(b, "batch");
+    hipStream_t s = own ? b->own_stream : (hipStream_t)stream;  // NULL = the default stream
+    if (s == b->stream) return 0;
+    SET_DEV(b);
+    HIP_TRY(hipStreamSynchronize(b->stream));  // work already queued on the old stream finishes first
+    b->stream = s;
+    return 0;
 }
 
 int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
@@ -884,6 +899,18 @@ int pbn_env_reset(pbn_batch* b, const pbn_envcfg* cfg_c, const uint8_t* mask) {
     if (int rc = run_init(b, cfg, d_mask, dv->reset_care, dv->reset_value)) return rc;
     HIP_TRY(hipStreamSynchronize(b->stream));
     return 0;
+}
+
+int pbn_env_reset_device(pbn_batch* b, const pbn_envcfg* cfg_c, const uint8_t* d_mask) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(cfg_c, "cfg");
+    pbn_envcfg* cfg = const_cast<pbn_envcfg*>(cfg_c);
+    if (cfg->net != b->net) return fail(PBN_E_INVALID, "envcfg belongs to another network");
+    if (cfg->H_reset < 1) return fail(PBN_E_STATE, "envcfg has no reset cubes (all_attractors[0])");
+    SET_DEV(b);
+    const pbn_envcfg::Dev* dv = cfg->on(b->device);
+    if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
+    return run_init(b, cfg, d_mask, dv->reset_care, dv->reset_value);
 }
 
 int pbn_set_n_steps(pbn_batch* b, const int64_t* n_steps) {

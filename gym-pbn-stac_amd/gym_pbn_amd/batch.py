@@ -285,6 +285,16 @@ class PBNBatch:
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8).reshape(self.n_envs)
         L.check(L.lib.pbn_env_reset(self._h, cfg.handle, L.ptr(m, L._u8p)))
 
+    def env_reset_device(self, cfg: EnvConfig, d_mask: int = 0):
+        """Asynchronous reset on the batch stream; ``d_mask``: device uint8 [B] pointer (0 = all)."""
+        L.check(L.lib.pbn_env_reset_device(self._h, cfg.handle, C.c_void_p(d_mask or None)))
+
+    def set_stream(self, stream=None):
+        """Run this batch's calls on a HIP stream handle (e.g. ``torch.cuda.current_stream().cuda_stream``,
+        0 being the default stream); ``None`` = the batch's own stream again."""
+        own = stream is None
+        L.check(L.lib.pbn_batch_set_stream(self._h, int(own), C.c_void_p(None if own or not stream else stream)))
+
     def set_n_steps(self, n_steps):
         a = np.ascontiguousarray(n_steps, dtype=np.int64).reshape(self.n_envs)
         L.check(L.lib.pbn_set_n_steps(self._h, L.ptr(a, L._i64p)))

@@ -1,0 +1,117 @@
+"""Device-resident vectorised multi-flip env for agents on the GPU (torch tensors in and out).
+
+``PBNTargetMultiEnv.step`` (``pbn_target_multi.py:119-154``) takes a torch action tensor and
+de-duplicates it with ``actions.unique()`` (``:120-121``): the reference is written for a
+torch agent (BDQ branches). Here the B envs, the agent's action tensor and every output stay
+on the GPU: the batch runs on torch's current stream (``pbn_batch_set_stream``), so the R6
+kernel orders with the policy's kernels without a host sync, and nothing crosses PCIe per
+step. Observations are unpacked from the packed state words with torch ops.
+
+Same transition, reward, termination and truncation as :class:`gym_pbn_amd.envs.VecPBNTargetMultiEnv`
+(one R6 launch per call; Philox draws keyed by the global env id); ``auto_reset`` resets the
+envs that ended, on the device, after their outputs were written (SB3 VecEnv convention; the
+reference env never resets itself).
+"""
+
+from __future__ import annotations
+
+from . import _lib as L
+from . import spaces
+from .batch import EnvConfig, Net, PBNBatch
+from .network import PredictorNetwork, load_network
+
+
+class TorchVecPBNTargetMultiEnv:
+    def __init__(self, network, attractors, n_envs: int, horizon: int = 100, device: int = 0, seed: int = 0,
+                 env_id_base: int = 0, update_cap: int = 1 << 20, auto_reset: bool = False):
+        import torch
+
+        if not isinstance(network, (PredictorNetwork, Net)):
+            network = load_network(network)
+        self.net = network if isinstance(network, Net) else Net(network)
+        self.num_envs = int(n_envs)
+        self.N, self.W = self.net.n_nodes, self.net.n_words
+        self.device = torch.device("cuda", device)
+        self.cfg = EnvConfig(self.net, attractors, horizon=horizon)
+        self.batch = PBNBatch(self.net, self.num_envs, device=device, env_id_base=env_id_base, seed=seed)
+        self.update_cap = int(update_cap)
+        self.auto_reset = bool(auto_reset)
+        self.observation_space = spaces.MultiBinary(self.N)  # pbn_target_multi.py:56-59
+        self.action_space = spaces.MultiDiscrete(self.N + 1)
+        B = self.num_envs
+        with torch.cuda.device(self.device):
+            self._words = torch.empty((B, self.W), dtype=torch.int64, device=self.device)
+            self._reward = torch.empty(B, dtype=torch.int32, device=self.device)
+            self._flags = torch.empty(B, dtype=torch.uint8, device=self.device)
+            self._nup = torch.empty(B, dtype=torch.int32, device=self.device)
+            self._shifts = torch.arange(64, dtype=torch.int64, device=self.device)
+        self._use_stream()
+
+    def _use_stream(self):
+        import torch
+
+        self.batch.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _bits(self, words):
+        """[B][W] int64 packed words -> [B][N] uint8 (bit i of word i // 64 = node i)."""
+        import torch
+
+        b = (words.unsqueeze(-1) >> self._shifts) & 1
+        return b.reshape(words.shape[0], self.W * 64)[:, : self.N].to(torch.uint8)
+
+    def observation_words(self):
+        self._use_stream()
+        self.batch.get_state_device(self._words.data_ptr())
+        return self._words
+
+    def reset(self, mask=None):
+        """Reset every env (``mask`` None) or the envs where the device bool/uint8 ``mask`` is set
+        (``reset``, :227-259, Philox draws); returns observations [B][N] uint8 on the device."""
+        import torch
+
+        self._use_stream()
+        if mask is None:
+            self.batch.env_reset_device(self.cfg, 0)
+        else:
+            # same stream as the kernel: the allocator cannot hand m's memory out before it ran
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            self.batch.env_reset_device(self.cfg, m.data_ptr())
+        return self._bits(self.observation_words())
+
+    def step(self, actions):
+        """``actions``: int tensor [B] or [B][A] of node + 1 values (0 = none), on the GPU.
+        Returns ``(obs [B][N] uint8, reward [B] int32, terminated [B] bool, truncated [B] bool,
+        info)`` as device tensors; ``info`` holds ``n_updates``, ``capped`` and ``obs_words``."""
+        import torch
+
+        a = actions
+        if a.dim() == 1:
+            a = a.unsqueeze(1)
+        a = a.to(device=self.device, dtype=torch.int32).contiguous()
+        if a.shape[0] != self.num_envs:
+            raise ValueError(f"actions for {a.shape[0]} envs, the batch has {self.num_envs}")
+        self._use_stream()
+        words = torch.empty((self.num_envs, self.W), dtype=torch.int64, device=self.device)
+        self.batch.env_step_multi_device(self.cfg, a.data_ptr(), a.shape[1], words.data_ptr(),
+                                         self._reward.data_ptr(), self._flags.data_ptr(), self._nup.data_ptr(),
+                                         offset=1, dedup=True, update_cap=self.update_cap)
+        flags = self._flags
+        term = (flags & L.FLAG_TERMINATED) != 0
+        trunc = (flags & L.FLAG_TRUNCATED) != 0
+        info = {"n_updates": self._nup.clone(), "capped": (flags & L.FLAG_CAPPED) != 0, "obs_words": words}
+        obs = self._bits(words)
+        reward = self._reward.clone()
+        if self.auto_reset:
+            done = (term | trunc).to(torch.uint8).contiguous()
+            self.batch.env_reset_device(self.cfg, done.data_ptr())
+        return obs, reward, term, trunc, info
+
+    def close(self):
+        import torch
+
+        torch.cuda.current_stream(self.device).synchronize()
+        self.batch.set_stream(None)
+        self.batch.close()
+
+
+__all__ = ["TorchVecPBNTargetMultiEnv"]

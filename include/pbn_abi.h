@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 4
+#define PBN_ABI_VERSION 5
 
 enum {
     PBN_OK = 0,
@@ -126,6 +126,10 @@ int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t e
                      pbn_batch **out);
 void pbn_batch_destroy(pbn_batch *b);
 int pbn_batch_get_info(const pbn_batch *b, pbn_batch_info *info);
+/* Run every later call of this batch on `stream` (a hipStream_t, e.g. torch's current stream, so
+ * kernels order with the caller's own work without host syncs; NULL = the default stream), or on
+ * the batch's own stream again (own != 0). Work queued on the previous stream is waited for first. */
+int pbn_batch_set_stream(pbn_batch *b, int own, void *stream);
 int pbn_sync(pbn_batch *b);
 
 /* ---- state I/O: Graph.setState / getState (base.py:364-366, 320-324), PBN.reset(state) (pbn.py:96-119) ---- */
@@ -160,6 +164,8 @@ void pbn_envcfg_destroy(pbn_envcfg *cfg);
 /* PBNTargetMultiEnv.reset (:227-259), Philox mode: envs with mask[e] != 0 (mask NULL = all)
  * get a reset cube chosen uniformly, '*' bits drawn fair, n_steps = 0. */
 int pbn_env_reset(pbn_batch *b, const pbn_envcfg *cfg, const uint8_t *mask);
+/* Same on the device, asynchronous: d_mask device uint8 [B] (NULL = all envs). */
+int pbn_env_reset_device(pbn_batch *b, const pbn_envcfg *cfg, const uint8_t *d_mask);
 int pbn_set_n_steps(pbn_batch *b, const int64_t *n_steps);  /* host [B] */
 int pbn_get_n_steps(pbn_batch *b, int64_t *n_steps);        /* host [B] */
 /* Host arrays: actions [B][A]; outputs obs [B][W], reward [B], flags [B], n_updates [B] (any may be NULL). */

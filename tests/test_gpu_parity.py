@@ -492,3 +492,35 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     if case in ("b28_gen_cap", "b28_grp4_cap", "b199_grp4_long"):
         assert (flags & 4).any() and not (flags & 4).all()  # some envs capped, some reached an attractor
     assert (nup > 1).any()
+
+
+def test_torch_vec_env_matches_host_vec_env(G):
+    """Device-resident env (torch tensors in/out, batch on torch's stream) == the host API env,
+    step for step, including on-device auto-reset of the envs that ended."""
+    import torch
+
+    from gym_pbn_amd.envs import VecPBNTargetMultiEnv
+    from gym_pbn_amd.torch_env import TorchVecPBNTargetMultiEnv
+
+    z = golden("r6_bittner28.npz")
+    att = cubes_to_attractors(z, 28)
+    B, A = 777, 2
+    tv = TorchVecPBNTargetMultiEnv("bittner28", att, B, horizon=3, seed=21, update_cap=4096, auto_reset=True)
+    hv = VecPBNTargetMultiEnv(load_network("bittner28"), att, B, horizon=3, seed=21, update_cap=4096, auto_reset=True)
+    assert tv.observation_space.shape == (28,)
+    o_t = tv.reset()
+    o_h = hv.reset()
+    assert o_t.is_cuda and o_t.dtype == torch.uint8 and np.array_equal(o_t.cpu().numpy(), o_h)
+    rng = np.random.default_rng(4)
+    for t in range(8):
+        a = rng.integers(0, 29, size=(B, A)).astype(np.int32)
+        a[rng.random(a.shape) < 0.6] = 0
+        ot, rt, tt, trt, it = tv.step(torch.from_numpy(a).cuda())
+        oh, rh, th, trh, ih = hv.step(a)
+        assert np.array_equal(ot.cpu().numpy(), oh), t
+        assert np.array_equal(rt.cpu().numpy(), rh) and np.array_equal(tt.cpu().numpy(), th), t
+        assert np.array_equal(trt.cpu().numpy(), trh), t
+        assert np.array_equal(it["n_updates"].cpu().numpy().view(np.uint32), ih["n_updates"]), t
+    assert trh.any()  # horizon 3: truncations (and auto-resets) happened
+    assert np.array_equal(tv.batch.get_state(), hv.batch.get_state())
+    tv.close()
