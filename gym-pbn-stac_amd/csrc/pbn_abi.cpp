@@ -510,6 +510,18 @@ int pbn_get_state_device(pbn_batch* b, void* dev_words) {
     return 0;
 }
 
+int pbn_unpack_bits_device(pbn_batch* b, const void* d_words, void* d_bits) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(d_bits, "d_bits");
+    SET_DEV(b);
+    const uint64_t total = b->B * (uint64_t)b->N;
+    const int grid = (int)std::min<uint64_t>((total + BLOCK - 1) / BLOCK, (uint64_t)b->n_cu * 32u);
+    int e = launch_unpack(d_words ? (const uint64_t*)d_words : b->d_state, (uint8_t*)d_bits, b->B, (uint32_t)b->N,
+                          (uint32_t)b->W, std::max(grid, 1), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_unpack launch: %s", hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
 static int run_init(pbn_batch* b, const pbn_envcfg* cfg, const void* d_mask, const void* care, const void* value) {
     InitArgs a{};
     a.state = b->d_state;

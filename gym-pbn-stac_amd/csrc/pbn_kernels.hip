@@ -1068,6 +1068,32 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream) {
     return launch(flip_fn(W), grid, 0, stream, &c, sizeof c);
 }
 
+// Packed state words [B][W] -> one byte per node [B][N] (Graph.getState as bytes, base.py:320-324):
+// one thread per output byte, so consecutive lanes write consecutive bytes (the rows of N bytes
+// are not 4-byte aligned) and read the same few words through L1/L2.
+__global__ __launch_bounds__(BLOCK) void k_unpack(const uint64_t* __restrict__ words, uint8_t* __restrict__ out,
+                                                  uint64_t total, uint32_t N, uint32_t W) {
+    if (total <= 0xFFFFFFFFull) {  // 32-bit index math (a 64-bit divide is a long software sequence)
+        for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < (uint32_t)total; k += gridDim.x * BLOCK) {
+            const uint32_t e = k / N, n = k - e * N;
+            out[k] = (uint8_t)((words[(uint64_t)e * W + (n >> 6)] >> (n & 63u)) & 1u);
+        }
+        return;
+    }
+    for (uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; k < total; k += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t e = k / N;
+        const uint32_t n = (uint32_t)(k - e * N);
+        out[k] = (uint8_t)((words[e * W + (n >> 6)] >> (n & 63u)) & 1u);
+    }
+}
+
+int launch_unpack(const uint64_t* words, uint8_t* out, uint64_t B, uint32_t N, uint32_t W, int grid, void* stream) {
+    const uint64_t total = B * N;
+    void* kargs[] = {(void*)&words, (void*)&out, (void*)&total, (void*)&N, (void*)&W};
+    return (int)hipLaunchKernel((const void*)k_unpack, dim3((unsigned)grid), dim3(BLOCK), kargs, 0,
+                                (hipStream_t)stream);
+}
+
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream) {
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast, a.grp)
                                               : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast, a.grp);

@@ -162,6 +162,7 @@ int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, in
 uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
+int launch_unpack(const uint64_t* words, uint8_t* out, uint64_t B, uint32_t N, uint32_t W, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout = 0);
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu);

@@ -105,6 +105,7 @@ SIGNATURES = {
     "pbn_env_reset": (C.c_int, [_vp, _vp, _u8p]),
     "pbn_env_reset_device": (C.c_int, [_vp, _vp, _vp]),
     "pbn_batch_set_stream": (C.c_int, [_vp, C.c_int, _vp]),
+    "pbn_unpack_bits_device": (C.c_int, [_vp, _vp, _vp]),
     "pbn_set_n_steps": (C.c_int, [_vp, _i64p]),
     "pbn_get_n_steps": (C.c_int, [_vp, _i64p]),
     "pbn_env_step_multi": (C.c_int, [_vp, _vp, _i32p, C.c_int, C.c_int, C.c_int, C.c_uint32, _u64p, _i32p, _u8p,

@@ -82,7 +82,7 @@ class Net:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and getattr(L, "lib", None) is not None:  # not at interpreter exit
             L.lib.pbn_net_destroy(h)
             self._h = None
 
@@ -139,7 +139,7 @@ class EnvConfig:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and getattr(L, "lib", None) is not None:
             L.lib.pbn_envcfg_destroy(h)
             self._h = None
 
@@ -208,7 +208,7 @@ class PBNBatch:
     # -- lifecycle --------------------------------------------------------
     def close(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and getattr(L, "lib", None) is not None:
             L.lib.pbn_batch_destroy(h)
             self._h = None
 
@@ -284,6 +284,10 @@ class PBNBatch:
     def env_reset(self, cfg: EnvConfig, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8).reshape(self.n_envs)
         L.check(L.lib.pbn_env_reset(self._h, cfg.handle, L.ptr(m, L._u8p)))
+
+    def unpack_bits_device(self, d_bits: int, d_words: int = 0):
+        """Device uint8 [B][N] node values from device words [B][W] (0 = the batch's state); async."""
+        L.check(L.lib.pbn_unpack_bits_device(self._h, C.c_void_p(d_words or None), C.c_void_p(d_bits)))
 
     def env_reset_device(self, cfg: EnvConfig, d_mask: int = 0):
         """Asynchronous reset on the batch stream; ``d_mask``: device uint8 [B] pointer (0 = all)."""

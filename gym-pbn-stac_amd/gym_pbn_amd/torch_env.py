@@ -5,7 +5,8 @@ de-duplicates it with ``actions.unique()`` (``:120-121``): the reference is writ
 torch agent (BDQ branches). Here the B envs, the agent's action tensor and every output stay
 on the GPU: the batch runs on torch's current stream (``pbn_batch_set_stream``), so the R6
 kernel orders with the policy's kernels without a host sync, and nothing crosses PCIe per
-step. Observations are unpacked from the packed state words with torch ops.
+step. Observations are unpacked from the packed state words by a small kernel (one byte per
+node, ``pbn_unpack_bits_device``).
 
 Same transition, reward, termination and truncation as :class:`gym_pbn_amd.envs.VecPBNTargetMultiEnv`
 (one R6 launch per call; Philox draws keyed by the global env id); ``auto_reset`` resets the
@@ -44,7 +45,6 @@ class TorchVecPBNTargetMultiEnv:
             self._reward = torch.empty(B, dtype=torch.int32, device=self.device)
             self._flags = torch.empty(B, dtype=torch.uint8, device=self.device)
             self._nup = torch.empty(B, dtype=torch.int32, device=self.device)
-            self._shifts = torch.arange(64, dtype=torch.int64, device=self.device)
         self._use_stream()
 
     def _use_stream(self):
@@ -52,12 +52,13 @@ class TorchVecPBNTargetMultiEnv:
 
         self.batch.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _bits(self, words):
-        """[B][W] int64 packed words -> [B][N] uint8 (bit i of word i // 64 = node i)."""
+    def _bits(self, words=None):
+        """[B][N] uint8 node values (k_unpack) from packed words [B][W] (None = the live state)."""
         import torch
 
-        b = (words.unsqueeze(-1) >> self._shifts) & 1
-        return b.reshape(words.shape[0], self.W * 64)[:, : self.N].to(torch.uint8)
+        out = torch.empty((self.num_envs, self.N), dtype=torch.uint8, device=self.device)
+        self.batch.unpack_bits_device(out.data_ptr(), 0 if words is None else words.data_ptr())
+        return out
 
     def observation_words(self):
         self._use_stream()
@@ -76,7 +77,7 @@ class TorchVecPBNTargetMultiEnv:
             # same stream as the kernel: the allocator cannot hand m's memory out before it ran
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
             self.batch.env_reset_device(self.cfg, m.data_ptr())
-        return self._bits(self.observation_words())
+        return self._bits()
 
     def step(self, actions):
         """``actions``: int tensor [B] or [B][A] of node + 1 values (0 = none), on the GPU.

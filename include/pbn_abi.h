@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 5
+#define PBN_ABI_VERSION 6
 
 enum {
     PBN_OK = 0,
@@ -137,6 +137,9 @@ int pbn_set_state(pbn_batch *b, const uint64_t *words);          /* host [B][W] 
 int pbn_get_state(pbn_batch *b, uint64_t *words);                /* host [B][W] */
 int pbn_set_state_device(pbn_batch *b, const void *dev_words);   /* device [B][W], same device */
 int pbn_get_state_device(pbn_batch *b, void *dev_words);
+/* One byte per node, device [B][N] uint8, from device words [B][W] (NULL = the batch's state);
+ * Graph.getState (base.py:320-324) for the whole batch without leaving the GPU. Asynchronous. */
+int pbn_unpack_bits_device(pbn_batch *b, const void *d_words, void *d_bits);
 /* Graph.genRandState (base.py:368-370) / PBN.reset(None) (pbn.py:105-118) in Philox mode */
 int pbn_randomize_state(pbn_batch *b);
 
