@@ -63,6 +63,21 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging for small transfers (single envs, small batches): pageable copies of a
+// few bytes cost several microseconds each in the runtime's staging path.
+struct PinBuf {
+    static constexpr size_t CAP = 64 * 1024;
+    uint8_t* p = nullptr;
+    bool ready() {
+        if (!p && hipHostMalloc((void**)&p, CAP, hipHostMallocDefault) != hipSuccess) p = nullptr;
+        return p != nullptr;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+    }
+};
+
 }  // namespace
 
 struct pbn_net {
@@ -141,6 +156,7 @@ struct pbn_batch {
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
+    PinBuf pin;                                           // staging for small host<->device copies
     DevBuf s_ssd_hist, s_ssd_tab;                         // SSD histogram + gap/target tables
     uint64_t ssd_iters = 0;                               // SSD iteration counter (Philox)
     DevBuf s_sync_tab;                                    // perturbation gap table
@@ -423,6 +439,7 @@ void pbn_batch_destroy(pbn_batch* b) {
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
                       &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab})
         d->release();
+    b->pin.release();
     if (b->own_stream) {
         (void)hipStreamSynchronize(b->stream);
         (void)hipStreamDestroy(b->own_stream);
@@ -475,12 +492,24 @@ static int check_state_words(const pbn_batch* b, const uint64_t* w) {
     return 0;
 }
 
+// host -> device through the pinned staging buffer when small (the caller syncs before reuse)
+static int h2d(pbn_batch* b, void* dst, const void* src, size_t bytes) {
+    if (bytes <= PinBuf::CAP && b->pin.ready()) {
+        HIP_TRY(hipStreamSynchronize(b->stream));  // the staging buffer may still feed an earlier copy
+        memcpy(b->pin.p, src, bytes);
+        HIP_TRY(hipMemcpyAsync(dst, b->pin.p, bytes, hipMemcpyHostToDevice, b->stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, b->stream));
+    }
+    return 0;
+}
+
 int pbn_set_state(pbn_batch* b, const uint64_t* words) {
     CHECK_NN(b, "batch");
     CHECK_NN(words, "words");
     if (int rc = check_state_words(b, words)) return rc;
     SET_DEV(b);
-    HIP_TRY(hipMemcpyAsync(b->d_state, words, 8 * (size_t)b->W * b->B, hipMemcpyHostToDevice, b->stream));
+    if (int rc = h2d(b, b->d_state, words, 8 * (size_t)b->W * b->B)) return rc;
     HIP_TRY(hipStreamSynchronize(b->stream));
     return 0;
 }
@@ -489,7 +518,14 @@ int pbn_get_state(pbn_batch* b, uint64_t* words) {
     CHECK_NN(b, "batch");
     CHECK_NN(words, "words");
     SET_DEV(b);
-    HIP_TRY(hipMemcpyAsync(words, b->d_state, 8 * (size_t)b->W * b->B, hipMemcpyDeviceToHost, b->stream));
+    const size_t bytes = 8 * (size_t)b->W * b->B;
+    if (bytes <= PinBuf::CAP && b->pin.ready()) {
+        HIP_TRY(hipMemcpyAsync(b->pin.p, b->d_state, bytes, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
+        memcpy(words, b->pin.p, bytes);
+        return 0;
+    }
+    HIP_TRY(hipMemcpyAsync(words, b->d_state, bytes, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     return 0;
 }
@@ -1032,11 +1068,29 @@ static int env_host_common(pbn_batch* b, pbn_envcfg* cfg, const int32_t* actions
     if (int rc = b->s_rew.ensure(4 * b->B)) return rc;
     if (int rc = b->s_flags.ensure(b->B)) return rc;
     if (int rc = b->s_nup.ensure(4 * b->B)) return rc;
-    HIP_TRY(hipMemcpyAsync(b->s_act.p, actions, ab, hipMemcpyHostToDevice, b->stream));
-    return 0;
+    return h2d(b, b->s_act.p, actions, ab);
 }
 
 static int env_host_out(pbn_batch* b, uint64_t* obs, int32_t* reward, uint8_t* flags, uint32_t* n_updates) {
+    const size_t so = 8 * (size_t)b->W * b->B, sr = 4 * b->B, sf = b->B, sn = 4 * b->B;
+    const size_t oo = 0, orr = oo + so, of = orr + sr, on = of + sf, oe = (on + sn + 3) & ~(size_t)3;
+    if (oe + 4 <= PinBuf::CAP && b->pin.ready()) {  // one pinned block, one sync
+        uint8_t* q = b->pin.p;
+        HIP_TRY(hipMemcpyAsync(q + oo, b->s_obs.p, so, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipMemcpyAsync(q + orr, b->s_rew.p, sr, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipMemcpyAsync(q + of, b->s_flags.p, sf, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipMemcpyAsync(q + on, b->s_nup.p, sn, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipMemcpyAsync(q + oe, b->d_error, 4, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
+        if (obs) memcpy(obs, q + oo, so);
+        if (reward) memcpy(reward, q + orr, sr);
+        if (flags) memcpy(flags, q + of, sf);
+        if (n_updates) memcpy(n_updates, q + on, sn);
+        int32_t err;
+        memcpy(&err, q + oe, 4);
+        if (err) return fail(PBN_E_RANGE, "an action was out of range");
+        return 0;
+    }
     if (obs) HIP_TRY(hipMemcpyAsync(obs, b->s_obs.p, 8 * (size_t)b->W * b->B, hipMemcpyDeviceToHost, b->stream));
     if (reward) HIP_TRY(hipMemcpyAsync(reward, b->s_rew.p, 4 * b->B, hipMemcpyDeviceToHost, b->stream));
     if (flags) HIP_TRY(hipMemcpyAsync(flags, b->s_flags.p, b->B, hipMemcpyDeviceToHost, b->stream));

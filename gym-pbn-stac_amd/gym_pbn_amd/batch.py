@@ -8,6 +8,8 @@ one ``base.Graph`` / ``PBN`` per env and parallelises only by processes,
 
 from __future__ import annotations
 
+import functools
+
 import ctypes as C
 from typing import Optional, Sequence
 
@@ -30,11 +32,17 @@ def pack_bits(bits) -> np.ndarray:
     return np.bitwise_or.reduce(b << shifts, axis=-1).astype(np.uint64)
 
 
+@functools.lru_cache(maxsize=64)
+def _bit_index(n: int):
+    idx = np.arange(n)
+    return idx // 64, (idx % 64).astype(np.uint64)
+
+
 def unpack_bits(words, n: int) -> np.ndarray:
     """[..., W] uint64 -> [..., N] uint8."""
     words = np.asarray(words, dtype=np.uint64)
-    idx = np.arange(n)
-    return ((words[..., idx // 64] >> (idx % 64).astype(np.uint64)) & np.uint64(1)).astype(np.uint8)
+    wi, sh = _bit_index(int(n))
+    return ((words[..., wi] >> sh) & np.uint64(1)).astype(np.uint8)
 
 
 class Net:

@@ -64,7 +64,7 @@ class Graph:
         self._initialised = True
 
     def getState(self) -> tuple:  # base.py:320-324
-        return tuple(int(x) for x in self._b.get_bits()[0])
+        return tuple(self._b.get_bits()[0].tolist())
 
     def getLabeledState(self) -> dict:  # base.py:314-318
         return dict(zip(self.getIDs(), self.getState()))
@@ -286,7 +286,7 @@ class PBNTargetMultiEnv:
 
     @property
     def graph_state(self) -> tuple:
-        return tuple(int(x) for x in self._v.batch.get_bits()[0])
+        return tuple(self._v.batch.get_bits()[0].tolist())
 
     def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):  # :227-259
         if options is not None and "state" in options:
@@ -312,7 +312,7 @@ class PBNTargetMultiEnv:
         self.n_steps += 1
         if flags[0] & L.FLAG_CAPPED:
             raise RuntimeError(f"update cap ({self._v.update_cap}) reached before an attracting state")
-        o = tuple(int(x) for x in unpack_bits(obs, self.network.n_nodes)[0])
+        o = tuple(unpack_bits(obs, self.network.n_nodes)[0].tolist())
         info = {"observation_idx": state_to_idx(o), "observation_dict": o, "n_updates": int(nup[0])}
         return o, int(rew[0]), bool(flags[0] & L.FLAG_TERMINATED), bool(flags[0] & L.FLAG_TRUNCATED), info
 
@@ -396,7 +396,7 @@ class PBNTargetEnv:
                                                                 offset=1, dedup=True, update_cap=self.update_cap)
             if flags[0] & L.FLAG_CAPPED:
                 raise RuntimeError(f"update cap ({self.update_cap}) reached before an attracting state")
-            obs = tuple(int(x) for x in unpack_bits(words, self.N)[0])
+            obs = tuple(unpack_bits(words, self.N)[0].tolist())
             n = int(nup[0])
         terminated = self.in_target(obs)
         reward = 20 if terminated else -5  # :303-326
