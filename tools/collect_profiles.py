@@ -27,6 +27,14 @@ check = {"kernel": "pbn::k_step<4, 1, 1, 0, 1024>", "launches": len(d), "warmup_
          "rocprof_avg_us_timed": sum(d[w:w + n]) / len(d[w:w + n]) / 1e3, "rocprof_avg_us_all": sum(d) / len(d) / 1e3,
          "bench_hip_event_avg_us": bench["roofline"]["avg_kernel_us"],
          "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (same defaults as the bench line)"}
+prof_line = G / "bench_prof.json"
+if prof_line.exists():  # bench.py's own HIP-event average in the profiled process (same launches)
+    pl = [l for l in prof_line.read_text().splitlines() if l.startswith("{")]
+    if pl:
+        check["profiled_run_hip_event_avg_us"] = json.loads(pl[-1])["roofline"]["avg_kernel_us"]
+        check["note"] = ("rocprof_avg_us_timed and profiled_run_hip_event_avg_us come from the same profiled "
+                         "process; bench_hip_event_avg_us is the unprofiled bench line (kernel tracing adds a "
+                         "completion signal per dispatch)")
 (P / f"{tag}_bench_trace_check.json").write_text(json.dumps(check, indent=1) + "\n")
 shutil.copy(G / "pmc_traffic.json", P / "pmc_traffic.json")
 for k in ("fetch", "write"):
@@ -38,6 +46,13 @@ bm = G / "beyond_mall.json"
 if bm.exists():
     ls = [l for l in bm.read_text().splitlines() if l.startswith("{")]
     (P / f"{tag}_beyond_mall_8m.json").write_text(json.dumps(json.loads(ls[-1])["beyond_mall_8m"], indent=1) + "\n")
+if (G / "prof_aux" / "aux_kernel_stats.csv").exists():
+    shutil.copy(G / "prof_aux" / "aux_kernel_stats.csv", P / f"{tag}_aux_kernel_stats.csv")
+for src, dst in (("aux.json", "aux_kernels.json"), ("torch_env.json", "torch_env.json"),
+                 ("single_env.json", "single_env.json")):
+    if (G / src).exists():
+        ls = [l for l in (G / src).read_text().splitlines() if l.startswith("{")]
+        (P / f"{tag}_{dst}").write_text(ls[-1] + "\n")
 for n in ("r6_131k", "r6_1m"):
     ls = [l for l in (G / f"{n}.json").read_text().splitlines() if l.startswith("{")]
     (P / f"{tag}_config5_{n[3:]}.json").write_text(ls[-1] + "\n")
