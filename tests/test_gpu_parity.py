@@ -524,3 +524,40 @@ def test_torch_vec_env_matches_host_vec_env(G):
     assert trh.any()  # horizon 3: truncations (and auto-resets) happened
     assert np.array_equal(tv.batch.get_state(), hv.batch.get_state())
     tv.close()
+
+
+def test_sb3_vec_env_adapter(G):
+    """SB3 VecEnv conventions over the batched multi-flip env: dones = terminated | truncated,
+    ended envs reset at once (obs = their first observation of the next episode), the last
+    observation in infos["terminal_observation"], truncations marked "TimeLimit.truncated"."""
+    from gym_pbn_amd.envs import VecPBNTargetMultiEnv
+    from gym_pbn_amd.sb3 import PBNVecEnv
+
+    z = golden("r6_bittner28.npz")
+    att = cubes_to_attractors(z, 28)
+    B = 300
+    ve = PBNVecEnv(VecPBNTargetMultiEnv(load_network("bittner28"), att, B, horizon=4, seed=2, update_cap=4096),
+                   n_action_slots=2)
+    twin = VecPBNTargetMultiEnv(load_network("bittner28"), att, B, horizon=4, seed=2, update_cap=4096)
+    assert ve.num_envs == B and ve.action_space.shape == (2,) and ve.observation_space.shape == (28,)
+    obs = ve.reset()
+    assert np.array_equal(obs, twin.reset())
+    rng = np.random.default_rng(8)
+    n_done = 0
+    for t in range(10):
+        a = rng.integers(0, 29, size=(B, 2))
+        a[rng.random(a.shape) < 0.7] = 0
+        obs, rew, done, infos = ve.step(a)
+        o, r, term, trunc, _ = twin.step(a)
+        assert np.array_equal(done, term | trunc) and np.allclose(rew, r) and rew.dtype == np.float32
+        for i in np.nonzero(done)[0]:
+            assert np.array_equal(infos[i]["terminal_observation"], o[i])
+            assert infos[i]["TimeLimit.truncated"] == bool(trunc[i] and not term[i])
+        if done.any():
+            fresh = twin.reset(done)
+            o = o.copy()
+            o[done] = fresh[done]
+            n_done += int(done.sum())
+        assert np.array_equal(obs, o), t
+    assert n_done > B  # the horizon of 4 ends every episode at least twice
+    ve.close()
