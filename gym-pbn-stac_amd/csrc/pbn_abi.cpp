@@ -153,6 +153,10 @@ struct pbn_batch {
     int step_block = 1024;  // threads per workgroup of the Philox step kernel (256 or 1024)
     int store_mode = STORE_DIRTY;
     int envs_per_thread = 2;  // K: envs each thread walks per launch (pipelined)
+    // R6 launch knobs (measurement / tests; read once at pbn_batch_create)
+    bool env_no_gen = false;  // PBNSIM_ENV_NO_GEN: no cooperative draw generation
+    int env_group = 0;        // PBNSIM_ENV_GROUP: lanes per env (1 = lane mode), 0 = by batch size
+    int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
@@ -399,6 +403,9 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PBN_E_HIP, "hipGetDeviceProperties"));
     b->n_cu = prop.multiProcessorCount;
     if (const char* sbv = getenv("PBNSIM_STEP_BLOCK")) b->step_block = atoi(sbv) == 256 ? 256 : 1024;
+    b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
+    if (const char* v = getenv("PBNSIM_ENV_GROUP")) b->env_group = std::max(1, atoi(v));
+    if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
     else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
         b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
@@ -996,21 +1003,20 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     if (!dv) return fail(PBN_E_NOMEM, "envcfg upload failed");
     // cooperative draw generation: predictor mix, Philox, record index fits the u16 entry
     int mode = (cfg->fast && !replay && b->net->kind == KIND_PREDICTOR_MIX && cfg->L.pmax <= 16 &&
-                b->net->N <= 512 && !getenv("PBNSIM_ENV_NO_GEN"))
+                b->net->N <= 512 && !b->env_no_gen)
                    ? 2
                    : cfg->fast;
     // group mode (k_env_grp: G lanes per env, G updates per round trip)
     int grp = 1;
     if (mode == 2 && b->net->N <= 256) {
-        grp = env_group_size(b);
-        if (const char* v = getenv("PBNSIM_ENV_GROUP")) grp = atoi(v);
+        grp = b->env_group ? b->env_group : env_group_size(b);
         if (grp != 2 && grp != 4 && grp != 8) grp = 1;
         if (grp > 1) mode = 3;
     }
     int bpc = 1;
     if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes, &bpc))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
-    if (const char* v = getenv("PBNSIM_ENV_BPC")) bpc = std::max(1, std::min(bpc, atoi(v)));  // tuning knob
+    if (b->env_bpc) bpc = std::min(bpc, b->env_bpc);
     EnvArgs a{};
     a.state = b->d_state;
     a.n_steps = b->d_nsteps;

@@ -351,9 +351,9 @@ def test_trajectory_collector_matches_host_api(G, monkeypatch, net_name, fused, 
     col.finish()
     assert gathered is None
     assert b1.info()["env_lanes"] == int(group)
+    monkeypatch.setenv("PBNSIM_ENV_GROUP", "1")  # read at batch creation
     b2 = G.PBNBatch(net, B, seed=77, env_id_base=123)
     b2.env_reset(cfg)
-    monkeypatch.setenv("PBNSIM_ENV_GROUP", "1")
     for t in range(T):
         obs, rew, flags, nup = b2.env_step_multi(cfg, acts[t], update_cap=1 << 14)
         assert np.array_equal(buf["obs"][t].cpu().numpy().view(np.uint64), obs), t

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of R6 env-kernel builds (measurement only): per-step and fused chunk throughput.
-# Usage: tools/env_ab.sh lib1.so lib2.so ...   (PBNSIM_ENV_PARK etc. pass through)
+# Usage: tools/env_ab.sh lib1.so lib2.so ...   (PBNSIM_ENV_* knobs pass through)
 for L in "$@"; do
   for B in 131072 1048576; do
     echo -n "$L B=$B step: "
