@@ -374,7 +374,7 @@ def main():
     if rank == 0:
         out["config2_bittner28"] = cfg2
         out["config5_r6"] = r6
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the host-core baseline: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(net, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist is not None:
