@@ -157,6 +157,7 @@ struct pbn_batch {
     bool env_no_gen = false;  // PBNSIM_ENV_NO_GEN: no cooperative draw generation
     int env_group = 0;        // PBNSIM_ENV_GROUP: lanes per env (1 = lane mode), 0 = by batch size
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
+    int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
@@ -406,6 +407,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
     if (const char* v = getenv("PBNSIM_ENV_GROUP")) b->env_group = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
+    if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
         b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
@@ -831,11 +833,15 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     a.gap_thr = flip_gap_thr ? d_gap : nullptr;
     a.gap_inv_log2 = flip_gap_thr ? gap_inv_log2(flip_gap_thr, b->N) : 0.0f;
     a.hist = (uint64_t*)b->s_ssd_hist.p;
+    // one wave per env while the batch is small against the chip (the reference's 300 resets)
+    a.wave = b->ssd_wave >= 0 ? b->ssd_wave : (b->B <= (uint64_t)b->n_cu * 16u ? 1 : 0);
     a.lds_bytes = ssd_layout(b->W, b->net->L.bytes, b->N, n_targets, &a);
     if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "SSD LDS footprint %u B too large", a.lds_bytes);
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
-    int e = launch_ssd(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
+    const int grid = a.wave ? (int)std::min<uint64_t>((b->B + BLOCK / 64 - 1) / (BLOCK / 64), (uint64_t)b->n_cu * 8u)
+                            : b->grid_for(b->B, b->bpc_base);
+    int e = launch_ssd(b->W, a, grid, b->stream);
     if (e) return fail(PBN_E_HIP, "k_ssd launch: %s", hipGetErrorString((hipError_t)e));
     if (int rc = b->ev_end(stop)) return rc;
     std::vector<uint64_t> h(nb);

@@ -143,6 +143,7 @@ struct SSDArgs {
     float gap_inv_log2;        // 1 / log2(1-p) estimated from the table (geo_gap's first guess)
     uint64_t* hist;            // [2^g] accumulated counts (device)
     uint32_t off_planes, off_gap, off_tbit, off_targets, off_hist, lds_bytes;
+    int32_t wave;              // 1: one wave per env (k_ssd_wave), small batches
 };
 
 struct SyncArgs {

@@ -92,6 +92,155 @@ __global__ __launch_bounds__(BLOCK) void k_ssd(SSDArgs a) {
         if (hist[k]) atomicAdd(reinterpret_cast<unsigned long long*>(a.hist) + k, (unsigned long long)hist[k]);
 }
 
+// ---------------------------------------------------------------- one wave per env
+// At the reference's own size (300 resets) the lane-per-env kernel leaves the chip idle and each
+// lane's 4,000 iterations run back to back (~4 us each: two Philox draws, the gap search, the
+// update). Here a wave owns an env: for each chunk of 64 iterations, lane k draws iteration k's
+// flip positions and transition (they do not depend on the state: Philox counters are the
+// iteration index), then lane 0 applies the 64 iterations in order -- bucket, flips, update --
+// from LDS. Same draws as k_ssd, so the same counts and final states.
+constexpr int SSD_FMAX = 12;  // flip positions kept per iteration; more -> lane 0 redraws them
+struct RowT {
+    uint32_t* base;  // the env's 2W dwords
+    __device__ __forceinline__ uint32_t get(uint32_t d) const { return base[d]; }
+    __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d] = v; }
+    __device__ __forceinline__ uint32_t bit(uint32_t i) const { return (get(i >> 5) >> (i & 31u)) & 1u; }
+};
+constexpr uint32_t SSD_WAVE_BYTES = 64 * 8 + 64 * 8 + 64 * 2 * SSD_FMAX + 64 + 16 * 8;  // per wave, see below
+
+template <int W, int KIND>
+__global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint32_t nb = 1u << a.n_targets;
+    uint32_t* gap = reinterpret_cast<uint32_t*>(lds + a.off_gap);
+    int16_t* tbit = reinterpret_cast<int16_t*>(lds + a.off_tbit);
+    uint16_t* targets = reinterpret_cast<uint16_t*>(lds + a.off_targets);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(lds + a.off_hist);
+    for (uint32_t k = threadIdx.x; k < N; k += BLOCK) {
+        gap[k] = a.gap_thr ? a.gap_thr[k] : 0xFFFFFFFFu;
+        tbit[k] = -1;
+    }
+    for (uint32_t k = threadIdx.x; k < nb; k += BLOCK) hist[k] = 0;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < (uint32_t)a.n_targets; j += BLOCK) {
+        targets[j] = (uint16_t)a.targets[j];
+        tbit[a.targets[j]] = (int16_t)(a.n_targets - 1 - (int)j);
+    }
+    __syncthreads();
+    const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+    uint8_t* wb = lds + a.off_planes + wv * SSD_WAVE_BYTES;
+    uint64_t* tr_a = reinterpret_cast<uint64_t*>(wb);                 // [64] record (mix) or k53 (table)
+    uint32_t* tr_i = reinterpret_cast<uint32_t*>(wb + 64 * 8);        // [64] node (u32, 8-B slots)
+    uint16_t* fpos = reinterpret_cast<uint16_t*>(wb + 64 * 16);       // [64][SSD_FMAX]
+    uint8_t* fcnt = wb + 64 * 16 + 64 * 2 * SSD_FMAX;                 // [64], SSD_FMAX + 1 = overflow
+    const RowT R{reinterpret_cast<uint32_t*>(wb + 64 * 16 + 64 * 2 * SSD_FMAX + 64)};  // 2W dwords
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
+        const uint64_t g = a.env_base + e;
+        if (lane < 2u * W) R.put(lane, reinterpret_cast<const uint32_t*>(a.state + e * W)[lane]);
+        wave_sync();
+        uint32_t bucket = 0, cur = 0, run = 0;
+        if (lane == 0) {
+            for (int j = 0; j < a.n_targets; ++j) bucket = (bucket << 1) | R.bit(targets[j]);
+            cur = bucket;
+        }
+        for (uint32_t t0 = 0; t0 < a.iters; t0 += 64) {
+            const uint32_t n = min(64u, a.iters - t0);
+            // ---- draws of iterations t0 .. t0 + n - 1, one per lane
+            if (lane < n) {
+                const uint64_t it = a.iter_base + t0 + lane;
+                uint32_t cnt = 0;
+                if (a.gap_thr)
+                    bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2,
+                                        [&](uint32_t pos) {
+                                            if (cnt < (uint32_t)SSD_FMAX) fpos[lane * SSD_FMAX + cnt] = (uint16_t)pos;
+                                            ++cnt;
+                                        });
+                fcnt[lane] = (uint8_t)min(cnt, (uint32_t)SSD_FMAX + 1u);
+                uint32_t w[4];
+                philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);
+                const uint32_t i = philox_node<KIND>(w[0], N);
+                const uint64_t k53 = k53_of(w[1], w[2]);
+                tr_i[2 * lane] = i;
+                if constexpr (KIND == KIND_PREDICTOR_MIX)
+                    tr_a[lane] = predictor_record(i, k53, lds, a.L);
+                else
+                    tr_a[lane] = k53;
+            }
+            wave_sync();
+            // ---- lane 0 applies them in order (eval.py:84-96)
+            if (lane == 0) {
+                for (uint32_t c = 0; c < n; ++c) {
+                    if (bucket != cur) {
+                        atomicAdd(&hist[cur], run);
+                        cur = bucket;
+                        run = 0;
+                    }
+                    ++run;
+                    auto flip = [&](uint32_t pos) {
+                        const uint32_t d = pos >> 5;
+                        R.put(d, R.get(d) ^ (1u << (pos & 31u)));
+                        const int tb = tbit[pos];
+                        if (tb >= 0) bucket ^= 1u << tb;
+                    };
+                    const uint32_t fc = fcnt[c];
+                    if (fc <= (uint32_t)SSD_FMAX) {
+                        for (uint32_t q = 0; q < fc; ++q) flip(fpos[c * SSD_FMAX + q]);
+                    } else {  // more flips than the buffer holds: draw them again here
+                        bernoulli_positions(a.seed, (uint32_t)(a.iter_base + t0 + c), STREAM_SSD_FLIP, g, gap, N,
+                                            a.gap_inv_log2, flip);
+                    }
+                    const uint32_t i = tr_i[2 * c];
+                    uint32_t changed;
+                    if constexpr (KIND == KIND_PREDICTOR_MIX) {
+                        const uint32_t d = i >> 5, sh = i & 31u;
+                        const uint32_t self = R.get(d);
+                        const uint32_t y = predictor_apply(R, i, self, tr_a[c]);
+                        const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
+                        R.put(d, nv);
+                        changed = nv != self;
+                    } else {
+                        changed = table_update_lds(R, i, tr_a[c], lds, a.L);
+                    }
+                    if (changed) {
+                        const int tb = tbit[i];
+                        if (tb >= 0) bucket ^= 1u << tb;
+                    }
+                }
+            }
+            wave_sync();
+        }
+        if (lane == 0) atomicAdd(&hist[cur], run);
+        if (lane < 2u * W) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = R.get(lane);
+        wave_sync();
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nb; k += BLOCK)
+        if (hist[k]) atomicAdd(reinterpret_cast<unsigned long long*>(a.hist) + k, (unsigned long long)hist[k]);
+}
+
+template <int KIND>
+static void* ssd_wave_fn(int W) {
+    switch (W) {
+        case 1: return (void*)k_ssd_wave<1, KIND>;
+        case 2: return (void*)k_ssd_wave<2, KIND>;
+        case 3: return (void*)k_ssd_wave<3, KIND>;
+        case 4: return (void*)k_ssd_wave<4, KIND>;
+        case 5: return (void*)k_ssd_wave<5, KIND>;
+        case 6: return (void*)k_ssd_wave<6, KIND>;
+        case 7: return (void*)k_ssd_wave<7, KIND>;
+        case 8: return (void*)k_ssd_wave<8, KIND>;
+    }
+    return nullptr;
+}
+
 template <int KIND>
 static void* ssd_fn(int W) {
     switch (W) {
@@ -110,8 +259,9 @@ static void* ssd_fn(int W) {
 static uint32_t a16(uint32_t x) { return (x + 15u) & ~15u; }
 
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a) {
-    a->off_planes = image_bytes;
-    a->off_gap = a16(a->off_planes + 8u * (uint32_t)W * BLOCK);
+    a->off_planes = image_bytes;  // lane mode: state planes; wave mode: per-wave chunk buffers + row
+    const uint32_t per_block = a->wave ? (BLOCK / 64) * SSD_WAVE_BYTES : 8u * (uint32_t)W * BLOCK;
+    a->off_gap = a16(a->off_planes + per_block);
     a->off_tbit = a16(a->off_gap + 4u * (uint32_t)n_nodes);
     a->off_targets = a16(a->off_tbit + 2u * (uint32_t)n_nodes);
     a->off_hist = a16(a->off_targets + 2u * (uint32_t)n_targets);
@@ -119,7 +269,9 @@ uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSD
 }
 
 int launch_ssd(int W, const SSDArgs& a, int grid, void* stream) {
-    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? ssd_fn<KIND_PREDICTOR_MIX>(W) : ssd_fn<KIND_PROB_TABLE>(W);
+    void* fn = a.wave ? (a.L.kind == KIND_PREDICTOR_MIX ? ssd_wave_fn<KIND_PREDICTOR_MIX>(W)
+                                                          : ssd_wave_fn<KIND_PROB_TABLE>(W))
+                      : (a.L.kind == KIND_PREDICTOR_MIX ? ssd_fn<KIND_PREDICTOR_MIX>(W) : ssd_fn<KIND_PROB_TABLE>(W));
     if (!fn) return (int)hipErrorInvalidValue;
     SSDArgs c = a;
     const uint32_t lds = c.lds_bytes;

@@ -40,14 +40,17 @@ def test_flip_gap_table_is_bernoulli_process():
 
 
 GPU_CASES = [("bittner28", [0, 1, 2, 3, 6, 7, 9], 3000, 0.01), ("bittner199", [0, 1, 2, 3, 4, 5, 6], 2000, 0.01),
-             ("tt200", [5, 50, 150], 1500, 0.02), ("bittner70", [1, 2], 1000, 0.0)]
+             ("tt200", [5, 50, 150], 1500, 0.02), ("bittner70", [1, 2], 1000, 0.0),
+             ("bittner199", [3, 9], 1000, 0.09)]  # ~18 flips per iteration: past the per-iteration buffer
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wave", ["0", "1"])  # one lane per env / one wave per env (draws by 64 lanes)
 @pytest.mark.parametrize("name,targets,iters,p", GPU_CASES)
-def test_ssd_matches_oracle(oracle_mod, name, targets, iters, p):
+def test_ssd_matches_oracle(oracle_mod, monkeypatch, wave, name, targets, iters, p):
     from gym_pbn_amd.batch import PBNBatch, flip_gap_table
 
+    monkeypatch.setenv("PBNSIM_SSD_WAVE", wave)
     net = load_network(name)
     B = 600
     b = PBNBatch(net, B, seed=17, env_id_base=5)
