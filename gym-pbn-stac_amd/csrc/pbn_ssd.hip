@@ -106,7 +106,8 @@ struct RowT {
     __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d] = v; }
     __device__ __forceinline__ uint32_t bit(uint32_t i) const { return (get(i >> 5) >> (i & 31u)) & 1u; }
 };
-constexpr uint32_t SSD_WAVE_BYTES = 64 * 8 + 64 * 8 + 64 * 2 * SSD_FMAX + 64 + 16 * 8;  // per wave, see below
+// per wave: LDS-row path 64*8 + 64*8 + 64*2*SSD_FMAX + 64 + 16*8 = 2,752 B; uniform path 64*17*4
+constexpr uint32_t SSD_WAVE_BYTES = 64 * 17 * 4;
 
 template <int W, int KIND>
 __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
@@ -142,6 +143,88 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    if constexpr (KIND == KIND_PREDICTOR_MIX) {
+        // Uniform apply: the env's 2W dwords live one per lane in a VGPR (lane d holds dword d),
+        // iteration c's draws stay in lane c's registers, and the whole wave walks the chain in
+        // lockstep with wave-uniform values -- v_readlane with scalar lane indices, a lane select
+        // to write a dword back, SALU arithmetic: no LDS round trip on the dependent chain.
+        auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+        auto wl = [lane](uint32_t v, uint32_t l, uint32_t old) { return lane == l ? v : old; };  // v, l uniform
+        // LDS reads at a uniform address return the same value in every lane: say so, so that the
+        // bucket bookkeeping stays in scalar registers
+        auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+        uint32_t* fm = reinterpret_cast<uint32_t*>(wb);  // [64][17]: per-iteration flip masks
+        uint32_t tmaskv = 0;  // lane d: target-node bits of dword d
+        for (int j = 0; j < a.n_targets; ++j)
+            if ((uint32_t)(targets[j] >> 5) == lane) tmaskv |= 1u << (targets[j] & 31u);
+        for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
+            const uint64_t g = a.env_base + e;
+            uint32_t rowv = lane < 2u * W ? reinterpret_cast<const uint32_t*>(a.state + e * W)[lane] : 0u;
+            auto bitv = [&](uint32_t nd) { return (rl(rowv, nd >> 5) >> (nd & 31u)) & 1u; };
+            uint32_t bucket = 0;
+            for (int j = 0; j < a.n_targets; ++j) bucket = (bucket << 1) | bitv(uni(targets[j]));
+            uint32_t cur = bucket, run = 0;
+            for (uint32_t t0 = 0; t0 < a.iters; t0 += 64) {
+                const uint32_t n = min(64u, a.iters - t0);
+                // ---- lane k draws iteration t0 + k: its flips folded into an XOR mask per dword (its
+                // own LDS row, stride 17 dwords: conflict-free) plus the bucket bits they toggle, and
+                // the transition's node and predictor record in registers
+                uint32_t my_i = 0, rec_lo = 0, rec_hi = 0, bdelta = 0;
+                uint32_t* fmr = fm + lane * 17u;
+                if (lane < n) {
+                    const uint64_t it = a.iter_base + t0 + lane;
+#pragma unroll
+                    for (int q = 0; q < 2 * W; ++q) fmr[q] = 0u;
+                    if (a.gap_thr)
+                        bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2,
+                                            [&](uint32_t pos) {
+                                                fmr[pos >> 5] ^= 1u << (pos & 31u);
+                                                const int tb = tbit[pos];
+                                                if (tb >= 0) bdelta ^= 1u << tb;
+                                            });
+                    uint32_t w[4];
+                    philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);
+                    my_i = philox_node<KIND>(w[0], N);
+                    const uint64_t rec = predictor_record(my_i, k53_of(w[1], w[2]), lds, a.L);
+                    rec_lo = (uint32_t)rec;
+                    rec_hi = (uint32_t)(rec >> 32);
+                }
+                wave_sync();
+                // ---- the wave applies iterations t0 .. t0 + n - 1 in order (eval.py:84-96)
+                const bool mine = lane < 2u * W;  // lanes holding a dword of the env
+                uint32_t fnext = mine ? fm[lane] : 0u;
+                for (uint32_t c = 0; c < n; ++c) {
+                    if (bucket != cur) {
+                        if (lane == 0) atomicAdd(&hist[cur], run);
+                        cur = bucket;
+                        run = 0;
+                    }
+                    ++run;
+                    const uint32_t f = fnext;  // iteration c's flips (read one iteration ahead)
+                    fnext = mine ? fm[min(c + 1, n - 1) * 17u + lane] : 0u;
+                    rowv ^= f;
+                    bucket ^= rl(bdelta, c);
+                    const uint32_t i = rl(my_i, c), lo = rl(rec_lo, c), hi = rl(rec_hi, c);
+                    const uint32_t x = (bitv(lo & 0xFFFFu) << 3) | (bitv(lo >> 16) << 2) | (bitv(hi & 0xFFFFu) << 1) |
+                                       bitv(i);
+                    const uint32_t y = (hi >> (16 + x)) & 1u;
+                    const uint32_t d = i >> 5, sh = i & 31u;
+                    const uint32_t wold = rl(rowv, d), wnew = (wold & ~(1u << sh)) | (y << sh);
+                    if (wnew != wold) {
+                        rowv = wl(wnew, d, rowv);
+                        if ((rl(tmaskv, d) >> sh) & 1u) bucket ^= 1u << uni((uint32_t)tbit[i]);
+                    }
+                }
+                wave_sync();  // the rows are rewritten by the next chunk's draws
+            }
+            if (lane == 0) atomicAdd(&hist[cur], run);
+            if (lane < 2u * W) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = rowv;
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nb; k += BLOCK)
+            if (hist[k]) atomicAdd(reinterpret_cast<unsigned long long*>(a.hist) + k, (unsigned long long)hist[k]);
+        return;
+    }
     for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
         const uint64_t g = a.env_base + e;
         if (lane < 2u * W) R.put(lane, reinterpret_cast<const uint32_t*>(a.state + e * W)[lane]);
