@@ -95,10 +95,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd(SSDArgs a) {
 // ---------------------------------------------------------------- one wave per env
 // At the reference's own size (300 resets) the lane-per-env kernel leaves the chip idle and each
 // lane's 4,000 iterations run back to back (~4 us each: two Philox draws, the gap search, the
-// update). Here a wave owns an env: for each chunk of 64 iterations, lane k draws iteration k's
-// flip positions and transition (they do not depend on the state: Philox counters are the
-// iteration index), then lane 0 applies the 64 iterations in order -- bucket, flips, update --
-// from LDS. Same draws as k_ssd, so the same counts and final states.
+// update). Here a wave owns an env and works in chunks of 64 iterations: lane k draws iteration
+// k's flip positions and transition (they do not depend on the state: Philox counters are the
+// iteration index). Predictor-mix networks then resolve the chunk in parallel (fixed point over
+// the chunk's update DAG, see below); truth-table networks let lane 0 apply the 64 iterations in
+// order -- bucket, flips, update -- from LDS. Same draws as k_ssd, so the same counts and states.
 constexpr int SSD_FMAX = 12;  // flip positions kept per iteration; more -> lane 0 redraws them
 struct RowT {
     uint32_t* base;  // the env's 2W dwords
@@ -106,8 +107,9 @@ struct RowT {
     __device__ __forceinline__ void put(uint32_t d, uint32_t v) const { base[d] = v; }
     __device__ __forceinline__ uint32_t bit(uint32_t i) const { return (get(i >> 5) >> (i & 31u)) & 1u; }
 };
-// per wave: LDS-row path 64*8 + 64*8 + 64*2*SSD_FMAX + 64 + 16*8 = 2,752 B; uniform path 64*17*4
-constexpr uint32_t SSD_WAVE_BYTES = 64 * 17 * 4;
+// per wave: LDS-row path 64*8 + 64*8 + 64*2*SSD_FMAX + 64 + 16*8 = 2,752 B; predictor-mix path
+// flips/prefixes [64][17] u32 + writer masks [512] u64 + base row [16] u32 = 8,512 B
+constexpr uint32_t SSD_WAVE_BYTES = 64 * 17 * 4 + 512 * 8 + 16 * 4;
 
 template <int W, int KIND>
 __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
@@ -144,80 +146,118 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
     };
     const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
     if constexpr (KIND == KIND_PREDICTOR_MIX) {
-        // Uniform apply: the env's 2W dwords live one per lane in a VGPR (lane d holds dword d),
-        // iteration c's draws stay in lane c's registers, and the whole wave walks the chain in
-        // lockstep with wave-uniform values -- v_readlane with scalar lane indices, a lane select
-        // to write a dword back, SALU arithmetic: no LDS round trip on the dependent chain.
-        auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
-        auto wl = [lane](uint32_t v, uint32_t l, uint32_t old) { return lane == l ? v : old; };  // v, l uniform
-        // LDS reads at a uniform address return the same value in every lane: say so, so that the
-        // bucket bookkeeping stays in scalar registers
-        auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-        uint32_t* fm = reinterpret_cast<uint32_t*>(wb);  // [64][17]: per-iteration flip masks
-        uint32_t tmaskv = 0;  // lane d: target-node bits of dword d
-        for (int j = 0; j < a.n_targets; ++j)
-            if ((uint32_t)(targets[j] >> 5) == lane) tmaskv |= 1u << (targets[j] & 31u);
+        // Parallel in time: lane c owns iteration t0 + c of a 64-iteration chunk. All draws
+        // (flips, node, predictor record) are independent of the state, so lane c has them before
+        // any update is applied; only the four operand values of its update depend on earlier
+        // iterations of the chunk. With the chunk's flips folded into prefix XORs (P_c = XOR of
+        // the flip masks of iterations <= c; the state seen by update c is base ^ P_c, base = the
+        // chunk-initial state with the updates < c written as y ^ P at their node), operand n of
+        // update c is either the initial bit (no earlier writer of n in the chunk) or the base
+        // bit yb_k stored by its last earlier writer k. The writers are known up front (a 64-bit
+        // writer mask per node), so the chunk is a DAG of boolean updates: iterate all 64 lanes
+        // at once (ballot of the yb bits, one 64-bit shift per operand) until nothing changes --
+        // one round per level of the chain instead of one serial step per iteration. The fixed
+        // point is unique (update c reads only writers < c), so the result equals the serial
+        // order of eval.py:84-96 bit for bit.
+        uint32_t* fm = reinterpret_cast<uint32_t*>(wb);                                   // [64][17] flips / P
+        unsigned long long* wm = reinterpret_cast<unsigned long long*>(wb + 64 * 17 * 4);  // [512] writers
+        uint32_t* row = reinterpret_cast<uint32_t*>(wb + 64 * 17 * 4 + 512 * 8);          // [16] base state
+        auto xor_scan = [lane](uint32_t v) {  // inclusive prefix XOR over the wave's lanes
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = (uint32_t)__shfl_up((int)v, o);
+                if (lane >= (uint32_t)o) v ^= u;
+            }
+            return v;
+        };
+        const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
         for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
             const uint64_t g = a.env_base + e;
             uint32_t rowv = lane < 2u * W ? reinterpret_cast<const uint32_t*>(a.state + e * W)[lane] : 0u;
-            auto bitv = [&](uint32_t nd) { return (rl(rowv, nd >> 5) >> (nd & 31u)) & 1u; };
-            uint32_t bucket = 0;
-            for (int j = 0; j < a.n_targets; ++j) bucket = (bucket << 1) | bitv(uni(targets[j]));
-            uint32_t cur = bucket, run = 0;
             for (uint32_t t0 = 0; t0 < a.iters; t0 += 64) {
                 const uint32_t n = min(64u, a.iters - t0);
-                // ---- lane k draws iteration t0 + k: its flips folded into an XOR mask per dword (its
-                // own LDS row, stride 17 dwords: conflict-free) plus the bucket bits they toggle, and
-                // the transition's node and predictor record in registers
-                uint32_t my_i = 0, rec_lo = 0, rec_hi = 0, bdelta = 0;
-                uint32_t* fmr = fm + lane * 17u;
-                if (lane < n) {
-                    const uint64_t it = a.iter_base + t0 + lane;
+                const bool live = lane < n;
+                uint32_t* fmr = fm + lane * 17u;  // own row, stride 17 dwords: conflict-free
+                for (uint32_t k = lane; k < N; k += 64) wm[k] = 0ull;
+                if (lane < 2u * W) row[lane] = rowv;
 #pragma unroll
-                    for (int q = 0; q < 2 * W; ++q) fmr[q] = 0u;
+                for (int q = 0; q < 2 * W; ++q) fmr[q] = 0u;
+                // ---- draws of iteration t0 + lane (same counters as k_ssd)
+                uint32_t i = 0, rec_lo = 0, rec_hi = 0;
+                if (live) {
+                    const uint64_t it = a.iter_base + t0 + lane;
                     if (a.gap_thr)
                         bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2,
-                                            [&](uint32_t pos) {
-                                                fmr[pos >> 5] ^= 1u << (pos & 31u);
-                                                const int tb = tbit[pos];
-                                                if (tb >= 0) bdelta ^= 1u << tb;
-                                            });
+                                            [&](uint32_t pos) { atomicXor(&fmr[pos >> 5], 1u << (pos & 31u)); });
                     uint32_t w[4];
                     philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);
-                    my_i = philox_node<KIND>(w[0], N);
-                    const uint64_t rec = predictor_record(my_i, k53_of(w[1], w[2]), lds, a.L);
+                    i = philox_node<KIND>(w[0], N);
+                    const uint64_t rec = predictor_record(i, k53_of(w[1], w[2]), lds, a.L);
                     rec_lo = (uint32_t)rec;
                     rec_hi = (uint32_t)(rec >> 32);
                 }
+                // ---- own flips -> prefix P (lane-private rows), bucket bits of the own flips
+                auto tbits = [&](const uint32_t* r) {  // target bits of a row, first target = MSB
+                    uint32_t v = 0;
+                    for (int j = 0; j < a.n_targets; ++j) {
+                        const uint32_t t = targets[j];
+                        v = (v << 1) | ((r[t >> 5] >> (t & 31u)) & 1u);
+                    }
+                    return v;
+                };
+                const uint32_t own_b = tbits(fmr);
+#pragma unroll
+                for (int q = 0; q < 2 * W; ++q) fmr[q] = xor_scan(fmr[q]);
+                if (live) atomicOr(&wm[i], 1ull << lane);
                 wave_sync();
-                // ---- the wave applies iterations t0 .. t0 + n - 1 in order (eval.py:84-96)
-                const bool mine = lane < 2u * W;  // lanes holding a dword of the env
-                uint32_t fnext = mine ? fm[lane] : 0u;
-                for (uint32_t c = 0; c < n; ++c) {
-                    if (bucket != cur) {
-                        if (lane == 0) atomicAdd(&hist[cur], run);
-                        cur = bucket;
-                        run = 0;
-                    }
-                    ++run;
-                    const uint32_t f = fnext;  // iteration c's flips (read one iteration ahead)
-                    fnext = mine ? fm[min(c + 1, n - 1) * 17u + lane] : 0u;
-                    rowv ^= f;
-                    bucket ^= rl(bdelta, c);
-                    const uint32_t i = rl(my_i, c), lo = rl(rec_lo, c), hi = rl(rec_hi, c);
-                    const uint32_t x = (bitv(lo & 0xFFFFu) << 3) | (bitv(lo >> 16) << 2) | (bitv(hi & 0xFFFFu) << 1) |
-                                       bitv(i);
-                    const uint32_t y = (hi >> (16 + x)) & 1u;
-                    const uint32_t d = i >> 5, sh = i & 31u;
-                    const uint32_t wold = rl(rowv, d), wnew = (wold & ~(1u << sh)) | (y << sh);
-                    if (wnew != wold) {
-                        rowv = wl(wnew, d, rowv);
-                        if ((rl(tmaskv, d) >> sh) & 1u) bucket ^= 1u << uni((uint32_t)tbit[i]);
-                    }
+                // ---- operands: last earlier writer (or the initial bit) and the P_c correction
+                const uint32_t nd[4] = {rec_lo & 0xFFFFu, rec_lo >> 16, rec_hi & 0xFFFFu, i};
+                uint32_t lw[4], has[4], cst[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const unsigned long long m = wm[nd[k]] & below;
+                    has[k] = m != 0ull;
+                    lw[k] = m ? 63u - (uint32_t)__clzll(m) : 0u;
+                    const uint32_t pc = (fmr[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
+                    const uint32_t init = (row[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
+                    cst[k] = (has[k] ? 0u : init) ^ pc;
                 }
-                wave_sync();  // the rows are rewritten by the next chunk's draws
+                const uint32_t tt = rec_hi >> 16, pself = (fmr[i >> 5] >> (i & 31u)) & 1u;
+                // ---- fixed point over the chunk's updates
+                unsigned long long B = 0ull;  // bit c: base bit stored by update c
+                for (uint32_t r = 0; r <= n; ++r) {
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) x = (x << 1) | ((((uint32_t)(B >> lw[k]) & has[k]) ^ cst[k]) & 1u);
+                    const uint32_t yb = ((tt >> x) ^ pself) & 1u;
+                    const unsigned long long Bn = __ballot(live && yb);
+                    if (Bn == B) break;
+                    B = Bn;
+                }
+                // ---- histogram: the bucket before iteration c's flips = base ^ P_{c-1} on the targets
+                if (live) {
+                    uint32_t bb = 0;
+                    for (int j = 0; j < a.n_targets; ++j) {
+                        const uint32_t t = targets[j];
+                        const unsigned long long m = wm[t] & below;
+                        const uint32_t v = m ? (uint32_t)(B >> (63u - (uint32_t)__clzll(m))) & 1u
+                                             : (row[t >> 5] >> (t & 31u)) & 1u;
+                        bb = (bb << 1) | v;
+                    }
+                    atomicAdd(&hist[bb ^ tbits(fmr) ^ own_b], 1u);
+                }
+                // ---- the last writer of each node stores its base bit; then base ^ P_{n-1}
+                if (live && (wm[i] >> lane) == 1ull) {
+                    const uint32_t bit = 1u << (i & 31u);
+                    if ((B >> lane) & 1ull)
+                        atomicOr(&row[i >> 5], bit);
+                    else
+                        atomicAnd(&row[i >> 5], ~bit);
+                }
+                wave_sync();
+                rowv = lane < 2u * W ? row[lane] ^ fm[(n - 1) * 17u + lane] : 0u;
+                wave_sync();  // rows and tables are rewritten by the next chunk
             }
-            if (lane == 0) atomicAdd(&hist[cur], run);
             if (lane < 2u * W) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = rowv;
         }
         __syncthreads();

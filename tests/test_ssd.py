@@ -41,7 +41,18 @@ def test_flip_gap_table_is_bernoulli_process():
 
 GPU_CASES = [("bittner28", [0, 1, 2, 3, 6, 7, 9], 3000, 0.01), ("bittner199", [0, 1, 2, 3, 4, 5, 6], 2000, 0.01),
              ("tt200", [5, 50, 150], 1500, 0.02), ("bittner70", [1, 2], 1000, 0.0),
-             ("bittner199", [3, 9], 1000, 0.09)]  # ~18 flips per iteration: past the per-iteration buffer
+             ("bittner199", [3, 9], 1000, 0.09),  # ~18 flips per iteration: past the per-iteration buffer
+             ("syn5", [0, 2, 4], 700, 0.05),  # 5 nodes: long in-chunk dependency chains (wave mode rounds)
+             ("syn500", [7, 300, 499], 600, 0.01)]  # W = 8
+
+
+def _net(name):
+    if name.startswith("syn"):
+        from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
+
+        n = int(name[3:])
+        return PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(n, 4, seed=n), name=name)
+    return load_network(name)
 
 
 @pytest.mark.gpu
@@ -51,7 +62,7 @@ def test_ssd_matches_oracle(oracle_mod, monkeypatch, wave, name, targets, iters,
     from gym_pbn_amd.batch import PBNBatch, flip_gap_table
 
     monkeypatch.setenv("PBNSIM_SSD_WAVE", wave)
-    net = load_network(name)
+    net = _net(name)
     B = 600
     b = PBNBatch(net, B, seed=17, env_id_base=5)
     b.randomize()
