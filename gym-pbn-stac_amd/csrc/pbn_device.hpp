@@ -267,6 +267,30 @@ __device__ __forceinline__ void bernoulli_positions(uint64_t seed, uint32_t c0, 
     }
 }
 
+// Same positions as bernoulli_positions, four gaps per Philox draw resolved together: the gap
+// searches of one draw are independent (only the running position is a prefix sum), so their
+// LDS round trips overlap. For flip rates where several flips per call are common (SSD noise).
+template <class F>
+__device__ __forceinline__ void bernoulli_positions_x4(uint64_t seed, uint32_t c0, uint32_t stream, uint64_t gid,
+                                                       const uint32_t* gap, uint32_t N, float inv_log2q,
+                                                       F&& on_pos) {
+    uint32_t pos = 0;
+    bool first = true;
+    for (uint32_t m = 0;; ++m) {
+        uint32_t w[4], gp[4];
+        philox_draw(seed, c0, m, gid, stream, w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gp[k] = geo_gap(w[k], gap, N, inv_log2q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pos = first ? gp[k] : pos + 1u + gp[k];
+            first = false;
+            if (pos >= N) return;
+            on_pos(pos);
+        }
+    }
+}
+
 template <int W, class P_t>
 __device__ __forceinline__ void to_plane(const P_t& P, const uint64_t (&s)[W]) {
 #pragma unroll

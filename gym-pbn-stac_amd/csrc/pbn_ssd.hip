@@ -171,6 +171,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
             return v;
         };
         const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
+        auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+        const int nt = a.n_targets;  // <= 12 (host check)
+        uint32_t tg[12];             // target nodes, wave-uniform
+#pragma unroll
+        for (int j = 0; j < 12; ++j) tg[j] = j < nt ? uni(targets[j]) : 0u;
         for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
             const uint64_t g = a.env_base + e;
             uint32_t rowv = lane < 2u * W ? reinterpret_cast<const uint32_t*>(a.state + e * W)[lane] : 0u;
@@ -187,8 +192,8 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                 if (live) {
                     const uint64_t it = a.iter_base + t0 + lane;
                     if (a.gap_thr)
-                        bernoulli_positions(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2,
-                                            [&](uint32_t pos) { atomicXor(&fmr[pos >> 5], 1u << (pos & 31u)); });
+                        bernoulli_positions_x4(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2,
+                                               [&](uint32_t pos) { atomicXor(&fmr[pos >> 5], 1u << (pos & 31u)); });
                     uint32_t w[4];
                     philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);
                     i = philox_node<KIND>(w[0], N);
@@ -199,10 +204,9 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                 // ---- own flips -> prefix P (lane-private rows), bucket bits of the own flips
                 auto tbits = [&](const uint32_t* r) {  // target bits of a row, first target = MSB
                     uint32_t v = 0;
-                    for (int j = 0; j < a.n_targets; ++j) {
-                        const uint32_t t = targets[j];
-                        v = (v << 1) | ((r[t >> 5] >> (t & 31u)) & 1u);
-                    }
+#pragma unroll
+                    for (int j = 0; j < 12; ++j)
+                        if (j < nt) v = (v << 1) | ((r[tg[j] >> 5] >> (tg[j] & 31u)) & 1u);
                     return v;
                 };
                 const uint32_t own_b = tbits(fmr);
@@ -237,13 +241,15 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                 // ---- histogram: the bucket before iteration c's flips = base ^ P_{c-1} on the targets
                 if (live) {
                     uint32_t bb = 0;
-                    for (int j = 0; j < a.n_targets; ++j) {
-                        const uint32_t t = targets[j];
-                        const unsigned long long m = wm[t] & below;
-                        const uint32_t v = m ? (uint32_t)(B >> (63u - (uint32_t)__clzll(m))) & 1u
-                                             : (row[t >> 5] >> (t & 31u)) & 1u;
-                        bb = (bb << 1) | v;
-                    }
+#pragma unroll
+                    for (int j = 0; j < 12; ++j)
+                        if (j < nt) {
+                            const uint32_t t = tg[j];
+                            const unsigned long long m = wm[t] & below;
+                            const uint32_t v = m ? (uint32_t)(B >> (63u - (uint32_t)__clzll(m))) & 1u
+                                                 : (row[t >> 5] >> (t & 31u)) & 1u;
+                            bb = (bb << 1) | v;
+                        }
                     atomicAdd(&hist[bb ^ tbits(fmr) ^ own_b], 1u);
                 }
                 // ---- the last writer of each node stores its base bit; then base ^ P_{n-1}
