@@ -82,6 +82,7 @@ struct PinBuf {
 
 struct pbn_net {
     int kind = 0, N = 0, W = 0;
+    int kmax = 0;                // truth-table networks: most inputs of one node
     std::vector<uint8_t> image;  // host copy of the LDS image
     NetLayout L{};
     std::mutex mu;
@@ -158,6 +159,7 @@ struct pbn_batch {
     int env_group = 0;        // PBNSIM_ENV_GROUP: lanes per env (1 = lane mode), 0 = by batch size
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
+    bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
@@ -289,6 +291,7 @@ static int build_table_image(const pbn_net_desc* d, pbn_net* n) {
         }
         sum_k += k;
         sum_t += (int64_t)1 << k;
+        n->kmax = std::max(n->kmax, (int)k);
     }
     NetLayout L{};
     L.off_node = 0;
@@ -408,6 +411,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_GROUP")) b->env_group = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
+    if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
         b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
@@ -835,6 +839,7 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     a.hist = (uint64_t*)b->s_ssd_hist.p;
     // one wave per env while the batch is small against the chip (the reference's 300 resets)
     a.wave = b->ssd_wave >= 0 ? b->ssd_wave : (b->B <= (uint64_t)b->n_cu * 16u ? 1 : 0);
+    a.dag = a.wave && !b->ssd_serial && (b->net->kind == PBN_KIND_PREDICTOR_MIX || b->net->kmax <= SSD_DAG_KMAX) ? 1 : 0;
     a.lds_bytes = ssd_layout(b->W, b->net->L.bytes, b->N, n_targets, &a);
     if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "SSD LDS footprint %u B too large", a.lds_bytes);
     hipEvent_t stop;

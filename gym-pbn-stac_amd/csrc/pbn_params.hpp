@@ -130,6 +130,8 @@ struct MTArgs {
     uint32_t* pos_np;
 };
 
+constexpr int SSD_DAG_KMAX = 6;  // truth-table nodes with more inputs: k_ssd_wave applies serially
+
 struct SSDArgs {
     uint64_t* state;           // [B][W]
     const void* img;           // network image
@@ -144,6 +146,8 @@ struct SSDArgs {
     uint64_t* hist;            // [2^g] accumulated counts (device)
     uint32_t off_planes, off_gap, off_tbit, off_targets, off_hist, lds_bytes;
     int32_t wave;              // 1: one wave per env (k_ssd_wave), small batches
+    int32_t dag;               // wave mode: resolve each 64-iteration chunk in parallel (predictor mix,
+                               // or truth tables with <= SSD_DAG_KMAX inputs per node)
 };
 
 struct SyncArgs {

@@ -97,10 +97,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd(SSDArgs a) {
 // lane's 4,000 iterations run back to back (~4 us each: two Philox draws, the gap search, the
 // update). Here a wave owns an env and works in chunks of 64 iterations: lane k draws iteration
 // k's flip positions and transition (they do not depend on the state: Philox counters are the
-// iteration index). Predictor-mix networks then resolve the chunk in parallel (fixed point over
-// the chunk's update DAG, see below); truth-table networks let lane 0 apply the 64 iterations in
-// order -- bucket, flips, update -- from LDS. Same draws as k_ssd, so the same counts and states.
-constexpr int SSD_FMAX = 12;  // flip positions kept per iteration; more -> lane 0 redraws them
+// iteration index). The chunk is then resolved in parallel (fixed point over the chunk's update
+// DAG, see below) for predictor-mix networks and truth-table networks with <= SSD_DAG_KMAX inputs
+// per node; otherwise lane 0 applies the 64 iterations in order -- bucket, flips, update -- from
+// LDS. Same draws as k_ssd, so the same counts and states.
+constexpr int SSD_FMAX = 12;  // serial apply: flip positions kept per iteration; more -> lane 0 redraws them
 struct RowT {
     uint32_t* base;  // the env's 2W dwords
     __device__ __forceinline__ uint32_t get(uint32_t d) const { return base[d]; }
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
-    if constexpr (KIND == KIND_PREDICTOR_MIX) {
+    if (a.dag) {
         // Parallel in time: lane c owns iteration t0 + c of a 64-iteration chunk. All draws
         // (flips, node, predictor record) are independent of the state, so lane c has them before
         // any update is applied; only the four operand values of its update depend on earlier
@@ -158,7 +159,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         // at once (ballot of the yb bits, one 64-bit shift per operand) until nothing changes --
         // one round per level of the chain instead of one serial step per iteration. The fixed
         // point is unique (update c reads only writers < c), so the result equals the serial
-        // order of eval.py:84-96 bit for bit.
+        // order of eval.py:84-96 bit for bit. Truth-table networks (node.py:31-38) take the same
+        // route when every node has <= 6 inputs: lane c turns its threshold row and k53 into a
+        // 2^k-bit table of y (k53 < thr[x] for every input pattern x), after which both kinds are
+        // "y = table bit x of the operand values".
+        constexpr int KOP = KIND == KIND_PREDICTOR_MIX ? 4 : SSD_DAG_KMAX;
         uint32_t* fm = reinterpret_cast<uint32_t*>(wb);                                   // [64][17] flips / P
         unsigned long long* wm = reinterpret_cast<unsigned long long*>(wb + 64 * 17 * 4);  // [512] writers
         uint32_t* row = reinterpret_cast<uint32_t*>(wb + 64 * 17 * 4 + 512 * 8);          // [16] base state
@@ -188,7 +193,10 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
 #pragma unroll
                 for (int q = 0; q < 2 * W; ++q) fmr[q] = 0u;
                 // ---- draws of iteration t0 + lane (same counters as k_ssd)
-                uint32_t i = 0, rec_lo = 0, rec_hi = 0;
+                uint32_t i = 0, nk = 0, nd[KOP];
+                uint64_t ytab = 0;  // bit x: y for operand pattern x
+#pragma unroll
+                for (int k = 0; k < KOP; ++k) nd[k] = 0;
                 if (live) {
                     const uint64_t it = a.iter_base + t0 + lane;
                     if (a.gap_thr)
@@ -197,9 +205,28 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                     uint32_t w[4];
                     philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);
                     i = philox_node<KIND>(w[0], N);
-                    const uint64_t rec = predictor_record(i, k53_of(w[1], w[2]), lds, a.L);
-                    rec_lo = (uint32_t)rec;
-                    rec_hi = (uint32_t)(rec >> 32);
+                    const uint64_t k53 = k53_of(w[1], w[2]);
+                    if constexpr (KIND == KIND_PREDICTOR_MIX) {
+                        // operands in0, in1, in2, self -> pattern bits 3..0 (predictor_apply)
+                        const uint64_t rec = predictor_record(i, k53, lds, a.L);
+                        nd[0] = (uint32_t)rec & 0xFFFFu;
+                        nd[1] = (uint32_t)(rec >> 16) & 0xFFFFu;
+                        nd[2] = (uint32_t)(rec >> 32) & 0xFFFFu;
+                        nd[3] = i;
+                        nk = 4;
+                        ytab = rec >> 48;
+                    } else {
+                        // operands = the node's inputs, first = MSB (table_eval_lds)
+                        const uint64_t info = reinterpret_cast<const uint64_t*>(lds + a.L.off_node)[i];
+                        const uint32_t toff = (uint32_t)info, ioff = (uint32_t)(info >> 32) & 0xFFFFu;
+                        nk = (uint32_t)(info >> 48) & 0xFFu;  // <= SSD_DAG_KMAX (host check)
+                        const uint16_t* in = reinterpret_cast<const uint16_t*>(lds + a.L.off_rec) + ioff;
+#pragma unroll
+                        for (int k = 0; k < KOP; ++k)
+                            if ((uint32_t)k < nk) nd[k] = in[k];
+                        const uint64_t* thr = reinterpret_cast<const uint64_t*>(lds + a.L.off_thr) + toff;
+                        for (uint32_t x = 0; x < (1u << nk); ++x) ytab |= (uint64_t)(k53 < thr[x]) << x;
+                    }
                 }
                 // ---- own flips -> prefix P (lane-private rows), bucket bits of the own flips
                 auto tbits = [&](const uint32_t* r) {  // target bits of a row, first target = MSB
@@ -215,10 +242,9 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                 if (live) atomicOr(&wm[i], 1ull << lane);
                 wave_sync();
                 // ---- operands: last earlier writer (or the initial bit) and the P_c correction
-                const uint32_t nd[4] = {rec_lo & 0xFFFFu, rec_lo >> 16, rec_hi & 0xFFFFu, i};
-                uint32_t lw[4], has[4], cst[4];
+                uint32_t lw[KOP], has[KOP], cst[KOP];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < KOP; ++k) {
                     const unsigned long long m = wm[nd[k]] & below;
                     has[k] = m != 0ull;
                     lw[k] = m ? 63u - (uint32_t)__clzll(m) : 0u;
@@ -226,14 +252,16 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                     const uint32_t init = (row[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
                     cst[k] = (has[k] ? 0u : init) ^ pc;
                 }
-                const uint32_t tt = rec_hi >> 16, pself = (fmr[i >> 5] >> (i & 31u)) & 1u;
+                const uint32_t pself = (fmr[i >> 5] >> (i & 31u)) & 1u;
                 // ---- fixed point over the chunk's updates
                 unsigned long long B = 0ull;  // bit c: base bit stored by update c
                 for (uint32_t r = 0; r <= n; ++r) {
                     uint32_t x = 0;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) x = (x << 1) | ((((uint32_t)(B >> lw[k]) & has[k]) ^ cst[k]) & 1u);
-                    const uint32_t yb = ((tt >> x) ^ pself) & 1u;
+                    for (int k = 0; k < KOP; ++k)
+                        if (KIND == KIND_PREDICTOR_MIX || (uint32_t)k < nk)
+                            x = (x << 1) | ((((uint32_t)(B >> lw[k]) & has[k]) ^ cst[k]) & 1u);
+                    const uint32_t yb = ((uint32_t)(ytab >> x) ^ pself) & 1u;
                     const unsigned long long Bn = __ballot(live && yb);
                     if (Bn == B) break;
                     B = Bn;

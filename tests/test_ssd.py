@@ -43,10 +43,17 @@ GPU_CASES = [("bittner28", [0, 1, 2, 3, 6, 7, 9], 3000, 0.01), ("bittner199", [0
              ("tt200", [5, 50, 150], 1500, 0.02), ("bittner70", [1, 2], 1000, 0.0),
              ("bittner199", [3, 9], 1000, 0.09),  # ~18 flips per iteration: past the per-iteration buffer
              ("syn5", [0, 2, 4], 700, 0.05),  # 5 nodes: long in-chunk dependency chains (wave mode rounds)
-             ("syn500", [7, 300, 499], 600, 0.01)]  # W = 8
+             ("syn500", [7, 300, 499], 600, 0.01),  # W = 8
+             ("tt8", [1, 3, 7], 900, 0.05),  # 8 nodes, 3 inputs each
+             ("ttk7_40", [0, 5, 39], 700, 0.02)]  # 7 inputs per node: past the chunk DAG's 6 (serial apply)
 
 
 def _net(name):
+    if name.startswith("ttk"):  # ttk<k>_<n>: synthetic truth-table PBN
+        from gym_pbn_amd.network import TruthTableNetwork, synthetic_truth_table_pbn
+
+        k, n = (int(v) for v in name[3:].split("_"))
+        return TruthTableNetwork.from_pbn_data(synthetic_truth_table_pbn(n, k, seed=n), name=name)
     if name.startswith("syn"):
         from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
 
@@ -56,12 +63,14 @@ def _net(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wave", ["0", "1"])  # one lane per env / one wave per env (draws by 64 lanes)
+# one lane per env / one wave per env (chunk resolved in parallel) / one wave per env, serial apply
+@pytest.mark.parametrize("mode", ["lane", "wave", "wave_serial"])
 @pytest.mark.parametrize("name,targets,iters,p", GPU_CASES)
-def test_ssd_matches_oracle(oracle_mod, monkeypatch, wave, name, targets, iters, p):
+def test_ssd_matches_oracle(oracle_mod, monkeypatch, mode, name, targets, iters, p):
     from gym_pbn_amd.batch import PBNBatch, flip_gap_table
 
-    monkeypatch.setenv("PBNSIM_SSD_WAVE", wave)
+    monkeypatch.setenv("PBNSIM_SSD_WAVE", "0" if mode == "lane" else "1")
+    monkeypatch.setenv("PBNSIM_SSD_SERIAL", "1" if mode == "wave_serial" else "0")
     net = _net(name)
     B = 600
     b = PBNBatch(net, B, seed=17, env_id_base=5)
