@@ -137,10 +137,12 @@ def config2_supplement(device):
         b.rollout(256)
     b.timing(0)
     rms, rl = b.timing_read()
+    lanes = b.info()["roll_lanes"]
     b.close()
     return {"workload": "Bittner-28, 65,536 envs, 1 GPU (BASELINE config 2)",
             "step_env_steps_per_s": B * n / (ms / 1e3), "step_us_per_launch": ms * 1e3 / max(launches, 1),
-            "rollout_updates_per_launch": 256, "rollout_node_updates_per_s": B * 256 * 5 / (rms / 1e3)}
+            "rollout_updates_per_launch": 256, "rollout_node_updates_per_s": B * 256 * 5 / (rms / 1e3),
+            "rollout_lanes_per_env": lanes}
 
 
 def r6_supplement(args, world, rank, device, dist):

@@ -160,6 +160,7 @@ struct pbn_batch {
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
+    int roll_group = 1;       // PBNSIM_ROLL_GROUP: lanes per env of the rollout kernel (default by size)
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
@@ -373,6 +374,22 @@ void pbn_net_destroy(pbn_net* n) {
     delete n;
 }
 
+// k_rollout_grp: predictor mix, N <= 256 (byte-packed node lists of a group)
+static bool roll_group_ok(const pbn_net* net) { return net->kind == PBN_KIND_PREDICTOR_MIX && net->N <= 256; }
+
+// Lanes per env of the rollout kernel by batch size: the largest G with B x G <= 512 lanes per CU
+// (8 waves per CU). Measured on MI355X (tools/rollout_group_sweep.py, node-updates/s): Bittner-28
+// 65,536 envs 114 G (lane) -> 145 G (G = 2); 16,384 envs 31 -> 74 G (G = 8); Bittner-200
+// 65,536 envs 164 -> 183 G (G = 2); from 131,072 envs on lane mode is as fast or faster (the
+// group kernel spends ~1.1x (G = 2) to ~2x (G = 4, 8) the VALU work per update).
+static int roll_group_size(const pbn_batch* b, const pbn_net* net) {
+    if (!roll_group_ok(net)) return 1;
+    const uint64_t lanes = (uint64_t)b->n_cu * 512u;
+    for (int g = 8; g >= 2; g /= 2)
+        if (b->B * (uint64_t)g <= lanes) return g;
+    return 1;
+}
+
 int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
                      pbn_batch** out) {
     CHECK_NN(net_c, "net");
@@ -406,14 +423,21 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     };
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PBN_E_HIP, "hipGetDeviceProperties"));
     b->n_cu = prop.multiProcessorCount;
-    if (const char* sbv = getenv("PBNSIM_STEP_BLOCK")) b->step_block = atoi(sbv) == 256 ? 256 : 1024;
+    if (const char* sbv = getenv("PBNSIM_STEP_BLOCK"))
+        b->step_block = atoi(sbv) == 256 ? 256 : 1024;
+    else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
+        b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
     if (const char* v = getenv("PBNSIM_ENV_GROUP")) b->env_group = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
-    else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
-        b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
+    // rollout lanes per env: 1 = k_rollout; 2/4/8 = k_rollout_grp (predictor mix, N <= 256)
+    b->roll_group = roll_group_size(b, net);
+    if (const char* v = getenv("PBNSIM_ROLL_GROUP")) {
+        const int g = atoi(v);
+        b->roll_group = (g == 2 || g == 4 || g == 8) && roll_group_ok(net) ? g : 1;
+    }
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(PBN_E_HIP, "hipStreamCreate"));
     b->own_stream = b->stream;
@@ -430,7 +454,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
     if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, b->step_block, &b->bpc_step)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
-    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, BLOCK, &b->bpc_roll, 1)))
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, BLOCK, &b->bpc_roll, 1, b->roll_group)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
     if (hipStreamSynchronize(b->stream) != hipSuccess) return bail(fail(PBN_E_HIP, "stream sync"));
     *out = b;
@@ -485,6 +509,7 @@ int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
     info->reset_count = b->reset_count;
     info->mt_ready = b->mt_ready;
     info->env_lanes = b->env_lanes;
+    info->roll_lanes = b->roll_group;
     return 0;
 }
 
@@ -649,9 +674,10 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
     // step mode: K envs per thread (their loads overlap); rollout: one env per lane up to the
     // resident grid -- its T updates are the work, and more lanes hide more LDS latency
     // (Bittner-28 @65,536 envs, T = 256: 115 vs 62 G updates/s with K = 2)
-    const bool rollout = T > 1 && !replay;  // k_rollout, 256-thread groups
+    const bool rollout = T > 1 && !replay;  // k_rollout (or k_rollout_grp), 256-thread groups
+    a.grp = rollout ? b->roll_group : 1;
     const uint64_t K = rollout ? 1u : (uint64_t)b->envs_per_thread;
-    const uint64_t lanes = (b->B + K - 1) / K;
+    const uint64_t lanes = rollout ? b->B * (uint64_t)a.grp : (b->B + K - 1) / K;
     const int sb = (replay || rollout) ? BLOCK : b->step_block;
     const int grid = replay    ? b->grid_for(lanes, b->bpc_base)
                      : rollout ? b->grid_for(lanes, b->bpc_roll, sb)

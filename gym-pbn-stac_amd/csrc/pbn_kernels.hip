@@ -693,6 +693,70 @@ struct GroupNodes {
     }
 };
 
+// One block of G consecutive updates of a group's env, lane k holding update k: node i, its
+// predictor record and the block-start values v of its operands (in0, in1, in2, self). Returns
+// y (node i's new value) and old (its value right before update k), exact in every lane.
+template <int G>
+struct GrpBlock {
+    uint32_t y = 0, old = 0;
+    uint32_t ip = 0;  // G == 2: the partner lane's node
+    GroupNodes<G> nodes;
+    __device__ __forceinline__ explicit GrpBlock(uint32_t i) : nodes(G == 2 ? 0u : i) {}
+    // update k is the last writer of node i among the first n_done updates of the block
+    __device__ __forceinline__ bool last(uint32_t i, uint32_t k, uint32_t n_done) const {
+        return G == 2 ? (k == 1 || n_done < 2 || ip != i) : nodes.match(i, k + 1, n_done) == 0u;
+    }
+};
+
+template <int G>
+__device__ __forceinline__ GrpBlock<G> grp_resolve(uint32_t i, uint64_t rec, const uint32_t (&in)[4],
+                                                   const uint32_t (&v)[4], uint32_t k, uint32_t gbase,
+                                                   uint32_t gmask) {
+    GrpBlock<G> b(i);
+    const uint32_t tt = (uint32_t)(rec >> 48);
+    auto tt_of = [&](const uint32_t (&x)[4]) { return (tt >> ((x[0] << 3) | (x[1] << 2) | (x[2] << 1) | x[3])) & 1u; };
+    if constexpr (G == 2) {
+        // pairs: lane 1 depends on lane 0 only where an input is lane 0's node
+        b.ip = (uint32_t)__builtin_amdgcn_mov_dpp((int)i, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        const uint32_t y0 = tt_of(v);  // exact in lane 0
+        const uint32_t yb = (uint32_t)__builtin_amdgcn_mov_dpp((int)y0, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
+        uint32_t x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = (k == 1 && in[q] == b.ip) ? yb : v[q];
+        b.y = tt_of(x);
+        b.old = x[3];
+    } else {
+        int32_t wr[4];  // last writer j < k of each input, or -1
+        bool dep = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t mm = b.nodes.match(in[q], 0, k);
+            wr[q] = mm ? 31 - __clz((int)mm) : -1;
+            dep |= mm != 0;
+        }
+        auto eval = [&](uint32_t Y, uint32_t* self_old) {
+            uint32_t x[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = wr[q] >= 0 ? (Y >> wr[q]) & 1u : v[q];
+            *self_old = x[3];
+            return tt_of(x);
+        };
+        b.y = eval(0u, &b.old);  // exact where no input has an in-block writer
+        if (__ballot(dep) != 0) {
+            // after round r lanes 0..r are exact, so round G - 1 at the latest changes nothing;
+            // a round that changes nothing has `old` computed from the final outputs
+#pragma unroll 1
+            for (int r = 0; r < G; ++r) {
+                const uint32_t Y = (uint32_t)(__ballot(b.y != 0u) >> gbase) & gmask;
+                const uint32_t yn = eval(Y, &b.old);
+                if (__ballot(yn != b.y) == 0) break;
+                b.y = yn;
+            }
+        }
+    }
+    return b;
+}
+
 template <int W, int G>
 __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
@@ -811,50 +875,8 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
         uint32_t v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = (row[in[q] >> 5] >> (in[q] & 31u)) & 1u;  // block-start values
-        const uint32_t tt = (uint32_t)(rec >> 48);
-        auto tt_of = [&](const uint32_t (&x)[4]) { return (tt >> ((x[0] << 3) | (x[1] << 2) | (x[2] << 1) | x[3])) & 1u; };
-        uint32_t y, old;  // node i's new value and its value before update k
-        uint32_t ip = 0;  // G == 2: the partner lane's node
-        GroupNodes<G> nodes(G == 2 ? 0u : i);
-        if constexpr (G == 2) {
-            // pairs: lane 1 depends on lane 0 only where an input is lane 0's node
-            ip = (uint32_t)__builtin_amdgcn_mov_dpp((int)i, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-            const uint32_t y0 = tt_of(v);  // exact in lane 0
-            const uint32_t yb = (uint32_t)__builtin_amdgcn_mov_dpp((int)y0, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
-            uint32_t x[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = (k == 1 && in[q] == ip) ? yb : v[q];
-            y = tt_of(x);
-            old = x[3];
-        } else {
-            int32_t wr[4];  // last writer j < k of each input, or -1
-            bool dep = false;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t mm = nodes.match(in[q], 0, k);
-                wr[q] = mm ? 31 - __clz((int)mm) : -1;
-                dep |= mm != 0;
-            }
-            auto eval = [&](uint32_t Y, uint32_t* self_old) {
-                uint32_t x[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) x[q] = wr[q] >= 0 ? (Y >> wr[q]) & 1u : v[q];
-                *self_old = x[3];
-                return tt_of(x);
-            };
-            y = eval(0u, &old);  // exact where no input has an in-block writer
-            if (__ballot(dep) != 0) {
-                // after round r lanes 0..r are exact, so round G - 1 at the latest changes nothing;
-                // a round that changes nothing has `old` computed from the final outputs
-#pragma unroll 1
-                for (int r = 0; r < G; ++r) {
-                    const uint32_t Y = (uint32_t)(__ballot(y != 0u) >> gbase) & gmask;
-                    const uint32_t yn = eval(Y, &old);
-                    if (__ballot(yn != y) == 0) break;
-                    y = yn;
-                }
-            }
-        }
+        const GrpBlock<G> blk = grp_resolve<G>(i, rec, in, v, k, gbase, gmask);
+        const uint32_t y = blk.y, old = blk.old;
         // mismatch counters after each update of the block (inclusive prefix over the group)
         const bool changed = y != old;
         uint32_t dl = changed ? (y ? nd.x : 0u - nd.x) : 0u;
@@ -885,7 +907,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
         const bool done = SM != 0u || used + n_done >= a.update_cap;
         const bool capped = SM == 0u;  // only meaningful when done
         // commit: the last writer of each node among the first n_done updates sets its bit
-        const bool last = G == 2 ? (k == 1 || n_done < 2 || ip != i) : nodes.match(i, k + 1, n_done) == 0u;
+        const bool last = blk.last(i, k, n_done);
         if (e >= 0 && k < n_done && y != v[3] && last) {
             if (y)
                 atomicOr(&row[i >> 5], 1u << (i & 31u));
@@ -936,10 +958,93 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ rollout, group mode
+// k_rollout with G lanes per env (predictor mix, N <= 256): each block of G consecutive updates
+// is resolved at once by grp_resolve (the same machinery as k_env_grp), the env's state kept as
+// one LDS row per group. Same Philox counters as k_rollout, so the same states. For batches too
+// small to give every SIMD several waves in lane mode (BASELINE config 2: 65,536 envs = one
+// wave per SIMD), where one env per lane is latency-bound on its own update chain.
+template <int W, int G>
+__global__ __launch_bounds__(BLOCK) void k_rollout_grp(StepArgs a) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    __syncthreads();
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+    const uint32_t lane = __lane_id();
+    const uint32_t k = lane & (G - 1);
+    const uint32_t gbase = lane & ~(uint32_t)(G - 1);
+    const uint32_t gmask = (1u << G) - 1u;
+    uint32_t* row = reinterpret_cast<uint32_t*>(lds + a.L.bytes) + (threadIdx.x / G) * (2 * W);
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    const uint64_t groups = (uint64_t)gridDim.x * (BLOCK / G);
+    // every group of a wave takes the same number of trips (ballots and wave syncs inside)
+    for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / G) + threadIdx.x / G;; e += groups) {
+        const bool live = e < a.B;
+        if (__ballot(live) == 0) break;
+        uint64_t s[W];
+        if (live) {
+            load_state<W>(a.state + e * W, s);
+            if (k == 0) {
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    row[2 * q] = (uint32_t)s[q];
+                    row[2 * q + 1] = (uint32_t)(s[q] >> 32);
+                }
+            }
+        }
+        wave_sync();
+        const uint64_t g = a.env_base + e;
+        for (uint32_t used = 0; used < a.T; used += G) {
+            const uint64_t u = a.update_base + used + k;
+            uint32_t w4[4];
+            philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w4);
+            const uint32_t i = philox_node<KIND_PREDICTOR_MIX>(w4[0], N);
+            const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, k53_of(w4[1], w4[2]), lds, a.L)];
+            const uint32_t in[4] = {(uint32_t)rec & 0xFFFFu, (uint32_t)(rec >> 16) & 0xFFFFu,
+                                    (uint32_t)(rec >> 32) & 0xFFFFu, i};
+            uint32_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = (row[in[q] >> 5] >> (in[q] & 31u)) & 1u;  // block-start values
+            const GrpBlock<G> blk = grp_resolve<G>(i, rec, in, v, k, gbase, gmask);
+            const uint32_t n_done = min((uint32_t)G, a.T - used);
+            // the last writer of each node among the block's valid updates sets its bit
+            if (live && k < n_done && blk.y != v[3] && blk.last(i, k, n_done)) {
+                if (blk.y)
+                    atomicOr(&row[i >> 5], 1u << (i & 31u));
+                else
+                    atomicAnd(&row[i >> 5], ~(1u << (i & 31u)));
+            }
+            wave_sync();
+        }
+        if (live && k == 0) {
+            uint64_t out[W];
+            bool diff = false;  // whole env, only if it differs (see k_step_single)
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                out[q] = (uint64_t)row[2 * q] | ((uint64_t)row[2 * q + 1] << 32);
+                diff |= out[q] != s[q];
+            }
+            if (diff) store_state<W>(a.state + e * W, out);
+        }
+        wave_sync();  // the row is rewritten by the group's next env
+    }
+}
+
 // ------------------------------------------------------------------ dispatch
 template <int W, int KIND>
-static void* step_fn(int store, int replay, int sb, int rollout) {
+static void* step_fn(int store, int replay, int sb, int rollout, int grp) {
     if (replay) return (void*)k_step<W, KIND, STORE_FULL, 1, BLOCK>;
+    if constexpr (KIND == KIND_PREDICTOR_MIX && W <= 4) {
+        if (rollout && grp == 2) return (void*)k_rollout_grp<W, 2>;
+        if (rollout && grp == 4) return (void*)k_rollout_grp<W, 4>;
+        if (rollout && grp == 8) return (void*)k_rollout_grp<W, 8>;
+    }
+    if (grp > 1) return nullptr;
     if (rollout) return sb == 1024 ? (void*)k_rollout<W, KIND, 1024> : (void*)k_rollout<W, KIND, BLOCK>;
     if (sb == 1024)
         return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0, 1024>
@@ -949,16 +1054,16 @@ static void* step_fn(int store, int replay, int sb, int rollout) {
 }
 
 template <int KIND>
-static void* step_fn_w(int W, int store, int replay, int sb, int rollout) {
+static void* step_fn_w(int W, int store, int replay, int sb, int rollout, int grp) {
     switch (W) {
-        case 1: return step_fn<1, KIND>(store, replay, sb, rollout);
-        case 2: return step_fn<2, KIND>(store, replay, sb, rollout);
-        case 3: return step_fn<3, KIND>(store, replay, sb, rollout);
-        case 4: return step_fn<4, KIND>(store, replay, sb, rollout);
-        case 5: return step_fn<5, KIND>(store, replay, sb, rollout);
-        case 6: return step_fn<6, KIND>(store, replay, sb, rollout);
-        case 7: return step_fn<7, KIND>(store, replay, sb, rollout);
-        case 8: return step_fn<8, KIND>(store, replay, sb, rollout);
+        case 1: return step_fn<1, KIND>(store, replay, sb, rollout, grp);
+        case 2: return step_fn<2, KIND>(store, replay, sb, rollout, grp);
+        case 3: return step_fn<3, KIND>(store, replay, sb, rollout, grp);
+        case 4: return step_fn<4, KIND>(store, replay, sb, rollout, grp);
+        case 5: return step_fn<5, KIND>(store, replay, sb, rollout, grp);
+        case 6: return step_fn<6, KIND>(store, replay, sb, rollout, grp);
+        case 7: return step_fn<7, KIND>(store, replay, sb, rollout, grp);
+        case 8: return step_fn<8, KIND>(store, replay, sb, rollout, grp);
     }
     return nullptr;
 }
@@ -1034,21 +1139,25 @@ static int launch(void* fn, int grid, uint32_t lds, void* stream, void* args, si
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
 }
 
-uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb) {
+uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb, int grp) {
+    if (grp > 1) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
     return image_bytes + 8u * (uint32_t)W * (uint32_t)sb;
 }
 
-static void* step_kernel(int W, int kind, int store_mode, int replay, int sb, int rollout) {
+static void* step_kernel(int W, int kind, int store_mode, int replay, int sb, int rollout, int grp) {
     if (replay) sb = BLOCK;
-    return kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay, sb, rollout)
-                                      : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay, sb, rollout);
+    return kind == KIND_PREDICTOR_MIX ? step_fn_w<KIND_PREDICTOR_MIX>(W, store_mode, replay, sb, rollout, grp)
+                                      : step_fn_w<KIND_PROB_TABLE>(W, store_mode, replay, sb, rollout, grp);
 }
 
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream) {
     if (replay) sb = BLOCK;
-    void* fn = step_kernel(W, a.L.kind, store_mode, replay, sb, !replay && a.T > 1);
+    const bool rollout = !replay && a.T > 1;
+    const int grp = rollout && a.grp > 1 ? a.grp : 1;
+    if (grp > 1) sb = BLOCK;
+    void* fn = step_kernel(W, a.L.kind, store_mode, replay, sb, rollout, grp);
     if (!fn) return (int)hipErrorInvalidValue;
-    const uint32_t lds = step_lds_bytes(W, a.L.bytes, sb);
+    const uint32_t lds = step_lds_bytes(W, a.L.bytes, sb, grp);
     if (lds > 64u * 1024u) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
@@ -1114,9 +1223,11 @@ static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
     return 0;
 }
 
-int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout) {
-    void* fn = step_kernel(W, kind, STORE_FULL, 0, sb, rollout);
-    return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb), blocks_per_cu);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout, int grp) {
+    if (grp > 1) sb = BLOCK;
+    void* fn = step_kernel(W, kind, STORE_FULL, 0, sb, rollout, grp);
+    if (!fn) return (int)hipErrorInvalidValue;
+    return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb, grp), blocks_per_cu);
 }
 
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp) {

@@ -49,6 +49,7 @@ struct StepArgs {
     uint32_t T;                  // updates per launch
     const uint32_t* replay_node; // [T][B] (replay mode)
     const uint64_t* replay_k53;  // [T][B]
+    int32_t grp;                 // rollout: lanes per env (1 = k_rollout; 2/4/8 = k_rollout_grp)
 };
 
 struct InitArgs {
@@ -164,12 +165,12 @@ struct SyncArgs {
 
 // Launchers (pbn_kernels.hip, pbn_mt.hip, pbn_ssd.hip, pbn_sync.hip). Return hipError_t as int.
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream);
-uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb);
+uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb, int grp = 1);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);
 int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_unpack(const uint64_t* words, uint8_t* out, uint64_t B, uint32_t N, uint32_t W, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
-int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout = 0);
+int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout = 0, int grp = 1);
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp);
 #ifndef PBN_ENV_CHUNK

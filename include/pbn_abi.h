@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 6
+#define PBN_ABI_VERSION 7
 
 enum {
     PBN_OK = 0,
@@ -82,6 +82,7 @@ typedef struct {
     uint32_t env_call_count, reset_count;
     int32_t mt_ready; /* 1 after pbn_mt_seed */
     int32_t env_lanes; /* last R6 env-step launch: 1 = one lane per env (k_env), 2/4/8 = lanes per env (k_env_grp) */
+    int32_t roll_lanes; /* rollout kernel: 1 = one lane per env (k_rollout), 2/4/8 = lanes per env (k_rollout_grp) */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).
@@ -124,7 +125,7 @@ void pbn_net_destroy(pbn_net *net);
 /* ---- batches of independent envs (the reference holds one Graph per env) ---- */
 /* Tuning knobs, read from the environment once here (measurement and tests only):
  * PBNSIM_STORE_MODE, PBNSIM_ENVS_PER_THREAD, PBNSIM_STEP_BLOCK (step kernel);
- * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL (SSD). */
+ * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env). */
 int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
                      pbn_batch **out);
 void pbn_batch_destroy(pbn_batch *b);

@@ -73,6 +73,31 @@ def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
     assert np.array_equal(b.get_state(), o.step_philox(init, 1234, 77, 0, 2 * T))
 
 
+@pytest.mark.parametrize("group", ["2", "4", "8"])
+@pytest.mark.parametrize("name", ["bittner28", "bittner199", "syn5", "tt200"])
+def test_rollout_group_mode_matches_oracle(G, oracle_mod, monkeypatch, group, name):
+    """k_rollout_grp (G lanes per env, blocks of G updates resolved at once): the same states as
+    the oracle for update counts that are not a multiple of G and ragged batches; tt200 (truth
+    tables) ignores the knob and stays in lane mode; syn5 has long in-block dependency chains."""
+    monkeypatch.setenv("PBNSIM_ROLL_GROUP", group)
+    if name == "syn5":
+        from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
+
+        net = PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(5, 4, seed=5), name="syn5")
+    else:
+        net = load_network(name)
+    o = oracle_mod.Oracle(net)
+    for B, T in ((1, 37), (65, 2), (1000, 61)):
+        b = G.PBNBatch(net, B, seed=31, env_id_base=9)
+        assert b.info()["roll_lanes"] == (1 if name == "tt200" else int(group))  # group mode really ran
+        b.randomize()
+        init = b.get_state()
+        b.rollout(T)
+        b.rollout(3)  # counters continue across calls
+        assert np.array_equal(b.get_state(), o.step_philox(init, 31, 9, 0, T + 3)), (B, T)
+        b.close()
+
+
 @pytest.mark.parametrize("name", ["bittner199", "bittner28"])
 def test_ragged_batches_and_zero_updates(G, oracle_mod, name):
     """Batch sizes that fill no wave / workgroup / pair evenly (1, 63, 65, 1023, 1025, 4097, 70001):
