@@ -161,6 +161,10 @@ struct pbn_batch {
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int roll_group = 1;       // PBNSIM_ROLL_GROUP: lanes per env of the rollout kernel (default by size)
+    bool step_graph_off = false;  // PBNSIM_STEP_GRAPH=0: step mode without HIP graphs
+    hipGraphExec_t step_graph = nullptr;  // STEP_GRAPH_K step launches + k_bump, captured once
+    bool step_graph_broken = false;       // capture or instantiation failed once: plain launches
+    DevBuf s_ubase;                       // device copy of update_count for graph replays
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
@@ -432,6 +436,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
+    if (const char* v = getenv("PBNSIM_STEP_GRAPH")) b->step_graph_off = atoi(v) == 0;
     // rollout lanes per env: 1 = k_rollout; 2/4/8 = k_rollout_grp (predictor mix, N <= 256)
     b->roll_group = roll_group_size(b, net);
     if (const char* v = getenv("PBNSIM_ROLL_GROUP")) {
@@ -474,8 +479,9 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
-                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab})
+                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase})
         d->release();
+    if (b->step_graph) (void)hipGraphExecDestroy(b->step_graph);
     b->pin.release();
     if (b->own_stream) {
         (void)hipStreamSynchronize(b->stream);
@@ -656,8 +662,10 @@ int pbn_flip(pbn_batch* b, const int32_t* actions, int A, int offset, int dedup)
     return 0;
 }
 
-static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int replay, const void* d_i, const void* d_k) {
+static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int replay, const void* d_i, const void* d_k,
+                       const uint64_t* ubase_dev = nullptr, bool timed = true) {
     StepArgs a{};
+    a.ubase_dev = ubase_dev;
     a.state = b->d_state;
     a.img = b->d_image;
     a.L = b->net->L;
@@ -668,8 +676,9 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
     a.T = T;
     a.replay_node = (const uint32_t*)d_i;
     a.replay_k53 = (const uint64_t*)d_k;
-    hipEvent_t stop;
-    if (int rc = b->ev_begin(&stop)) return rc;
+    hipEvent_t stop = nullptr;
+    if (timed)
+        if (int rc = b->ev_begin(&stop)) return rc;
     int store = (T == 1 && !replay) ? b->store_mode : STORE_FULL;
     // step mode: K envs per thread (their loads overlap); rollout: one env per lane up to the
     // resident grid -- its T updates are the work, and more lanes hide more LDS latency
@@ -684,13 +693,56 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
                                : b->grid_for(lanes, b->bpc_step, sb);
     int e = launch_step(b->W, a, store, replay, sb, grid, b->stream);
     if (e) return fail(PBN_E_HIP, "k_step launch: %s", hipGetErrorString((hipError_t)e));
-    return b->ev_end(stop);
+    return timed ? b->ev_end(stop) : 0;
+}
+
+// Step mode is launch-bound between kernels (one HBM pass each): runs of STEP_GRAPH_K launches
+// go out as one captured HIP graph -- the same kernels with the same arguments, except that the
+// update counter comes from device memory (*ubase + k for launch k; k_bump adds STEP_GRAPH_K
+// at the end of the graph), so one instantiated graph serves every replay.
+constexpr uint32_t STEP_GRAPH_K = 64;
+
+static bool step_graph_ready(pbn_batch* b) {
+    if (b->step_graph) return true;
+    if (b->step_graph_broken || b->step_graph_off || !b->stream) return false;  // the null stream cannot capture
+    if (b->s_ubase.ensure(64)) return false;
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    bool launched = ok;
+    for (uint32_t k = 0; launched && k < STEP_GRAPH_K; ++k)
+        launched = step_launch(b, 1, k, 0, nullptr, nullptr, (const uint64_t*)b->s_ubase.p, false) == 0;
+    if (launched) launched = launch_bump((uint64_t*)b->s_ubase.p, STEP_GRAPH_K, b->stream) == 0;
+    if (ok) ok = hipStreamEndCapture(b->stream, &g) == hipSuccess && launched && g;
+    if (ok) ok = hipGraphInstantiate(&b->step_graph, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok) {
+        b->step_graph = nullptr;
+        b->step_graph_broken = true;
+        (void)hipGetLastError();  // the failed capture is not the caller's error
+        g_err.clear();
+    }
+    return ok;
 }
 
 int pbn_step(pbn_batch* b, uint32_t n_updates) {
     CHECK_NN(b, "batch");
     SET_DEV(b);
-    for (uint32_t t = 0; t < n_updates; t++) {
+    uint32_t t = 0;
+    if (n_updates >= STEP_GRAPH_K && b->timing != 1 && step_graph_ready(b)) {
+        // device counter <- update_count (two 32-bit memsets: stream-ordered, no host buffer)
+        uint32_t* c = (uint32_t*)b->s_ubase.p;
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c, (int)(uint32_t)b->update_count, 1, b->stream));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c + 1), (int)(uint32_t)(b->update_count >> 32), 1, b->stream));
+        for (; t + STEP_GRAPH_K <= n_updates; t += STEP_GRAPH_K) {
+            hipEvent_t stop;
+            if (int rc = b->ev_begin(&stop)) return rc;
+            if (b->timing == 2) b->region_launches += STEP_GRAPH_K - 1;  // ev_begin counted one
+            HIP_TRY(hipGraphLaunch(b->step_graph, b->stream));
+            if (int rc = b->ev_end(stop)) return rc;
+            b->update_count += STEP_GRAPH_K;
+        }
+    }
+    for (; t < n_updates; t++) {
         if (int rc = step_launch(b, 1, b->update_count, 0, nullptr, nullptr)) return rc;
         b->update_count++;
     }

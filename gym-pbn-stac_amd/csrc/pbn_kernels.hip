@@ -44,7 +44,8 @@ namespace pbn {
 template <int W, int KIND, int STORE, int SB>
 __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, uint64_t e, uint64_t stride,
                                               uint64_t (&cur)[W], uint32_t N) {
-    const uint64_t u = a.update_base;
+    // graph replays read the batch's update counter from device memory (k_bump advances it)
+    const uint64_t u = a.update_base + (a.ubase_dev ? *a.ubase_dev : 0ull);
     const uint64_t po = stride;  // second env of the pair (adjacent envs measured slower: 8.2 vs 7.8 us)
     uint64_t nxt[W];
     uint32_t i0 = 0, i1 = 0;
@@ -1165,6 +1166,16 @@ int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, in
     StepArgs c = a;
     void* kargs[] = {&c};
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3((unsigned)sb), kargs, lds, (hipStream_t)stream);
+}
+
+// Advances the device-side update counter by k at the end of a captured run of step launches.
+__global__ void k_bump(uint64_t* p, uint64_t k) {
+    if (threadIdx.x == 0) p[threadIdx.x] += k;
+}
+
+int launch_bump(uint64_t* p, uint64_t k, void* stream) {
+    void* kargs[] = {(void*)&p, (void*)&k};
+    return (int)hipLaunchKernel((const void*)k_bump, dim3(1), dim3(64), kargs, 0, (hipStream_t)stream);
 }
 
 int launch_init(int W, const InitArgs& a, int grid, void* stream) {

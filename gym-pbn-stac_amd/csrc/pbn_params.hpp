@@ -50,6 +50,7 @@ struct StepArgs {
     const uint32_t* replay_node; // [T][B] (replay mode)
     const uint64_t* replay_k53;  // [T][B]
     int32_t grp;                 // rollout: lanes per env (1 = k_rollout; 2/4/8 = k_rollout_grp)
+    const uint64_t* ubase_dev;   // step mode in a HIP graph: update counter = *ubase_dev + update_base
 };
 
 struct InitArgs {
@@ -164,6 +165,7 @@ struct SyncArgs {
 };
 
 // Launchers (pbn_kernels.hip, pbn_mt.hip, pbn_ssd.hip, pbn_sync.hip). Return hipError_t as int.
+int launch_bump(uint64_t* p, uint64_t k, void* stream);
 int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, int grid, void* stream);
 uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb, int grp = 1);
 int launch_init(int W, const InitArgs& a, int grid, void* stream);

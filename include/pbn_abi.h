@@ -125,7 +125,8 @@ void pbn_net_destroy(pbn_net *net);
 /* ---- batches of independent envs (the reference holds one Graph per env) ---- */
 /* Tuning knobs, read from the environment once here (measurement and tests only):
  * PBNSIM_STORE_MODE, PBNSIM_ENVS_PER_THREAD, PBNSIM_STEP_BLOCK (step kernel);
- * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env). */
+ * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
+ * PBNSIM_STEP_GRAPH=0 (pbn_step without HIP graphs). */
 int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
                      pbn_batch **out);
 void pbn_batch_destroy(pbn_batch *b);
@@ -154,7 +155,9 @@ int pbn_randomize_state(pbn_batch *b);
 int pbn_flip(pbn_batch *b, const int32_t *actions, int A, int offset, int dedup);
 
 /* ---- the hot path: Graph.step (base.py:306-312) / PBN.step (pbn.py:129-133) ---- */
-/* Philox mode, n_updates launches of one update each (state round-trips HBM). */
+/* Philox mode, n_updates launches of one update each (state round-trips HBM). Runs of 64
+ * launches are replayed from one captured HIP graph (not on the null stream, nor with
+ * per-launch timing); results are identical either way. */
 int pbn_step(pbn_batch *b, uint32_t n_updates);
 /* Philox mode, one launch applying n_updates in registers; bit-identical to pbn_step. */
 int pbn_rollout(pbn_batch *b, uint32_t n_updates);

@@ -73,6 +73,32 @@ def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
     assert np.array_equal(b.get_state(), o.step_philox(init, 1234, 77, 0, 2 * T))
 
 
+@pytest.mark.parametrize("graph", ["1", "0"])
+@pytest.mark.parametrize("name", ["bittner199", "tt200"])
+def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name):
+    """pbn_step sends runs of 64 launches as one captured HIP graph (update counter read from
+    device memory): replays continue the counter exactly, across calls and mixed with plain
+    launches and rollouts; region timing still counts every launch."""
+    monkeypatch.setenv("PBNSIM_STEP_GRAPH", graph)
+    net = load_network(name)
+    o = oracle_mod.Oracle(net)
+    B = 5000
+    b = G.PBNBatch(net, B, seed=71, env_id_base=13)
+    b.randomize()
+    init = b.get_state()
+    b.step(64 * 3 + 7)  # three replays + seven plain launches
+    b.rollout(5)
+    b.step(64)
+    assert np.array_equal(b.get_state(), o.step_philox(init, 71, 13, 0, 64 * 4 + 12))
+    b.timing(2)
+    b.step(128)
+    b.timing(0)
+    ms, launches = b.timing_read()
+    assert launches == 128 and ms > 0
+    assert np.array_equal(b.get_state(), o.step_philox(init, 71, 13, 0, 64 * 6 + 12))
+    b.close()
+
+
 @pytest.mark.parametrize("group", ["2", "4", "8"])
 @pytest.mark.parametrize("name", ["bittner28", "bittner199", "syn5", "tt200"])
 def test_rollout_group_mode_matches_oracle(G, oracle_mod, monkeypatch, group, name):
