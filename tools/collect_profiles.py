@@ -53,6 +53,10 @@ for src, dst in (("aux.json", "aux_kernels.json"), ("torch_env.json", "torch_env
     if (G / src).exists():
         ls = [l for l in (G / src).read_text().splitlines() if l.startswith("{")]
         (P / f"{tag}_{dst}").write_text(ls[-1] + "\n")
+for src in ("rollout_group_sweep.txt", "ssd_time.txt"):  # text tables of the measurement helpers
+    if (G / src).exists():
+        ls = [l for l in (G / src).read_text().splitlines() if "=" in l and not l.startswith("/opt")]
+        (P / f"{tag}_{src}").write_text("\n".join(ls) + "\n")
 for n in ("r6_131k", "r6_1m"):
     ls = [l for l in (G / f"{n}.json").read_text().splitlines() if l.startswith("{")]
     (P / f"{tag}_config5_{n[3:]}.json").write_text(ls[-1] + "\n")

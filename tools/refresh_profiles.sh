@@ -18,3 +18,5 @@ step aux timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv 
 echo auxjson; timeout -k 10 300 python tools/bench_aux.py > gpurun_out/aux.json || exit $?
 echo torchenv; timeout -k 10 200 python tools/bench_torch_env.py 1048576 10 > gpurun_out/torch_env.json || exit $?
 echo single; timeout -k 10 200 python tools/bench_single_env.py > gpurun_out/single_env.json || exit $?
+echo rgsweep; timeout -k 10 200 python tools/rollout_group_sweep.py > gpurun_out/rollout_group_sweep.txt || exit $?
+echo ssdtime; timeout -k 10 200 python tools/ssd_time.py > gpurun_out/ssd_time.txt || exit $?
