@@ -201,7 +201,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                     const uint64_t it = a.iter_base + t0 + lane;
                     if (a.gap_thr)
                         bernoulli_positions_x4(a.seed, (uint32_t)it, STREAM_SSD_FLIP, g, gap, N, a.gap_inv_log2,
-                                               [&](uint32_t pos) { atomicXor(&fmr[pos >> 5], 1u << (pos & 31u)); });
+                                               [&](uint32_t pos) { fmr[pos >> 5] ^= 1u << (pos & 31u); });
                     uint32_t w[4];
                     philox_draw(a.seed, (uint32_t)it, (uint32_t)(it >> 32), g, STREAM_SSD, w);
                     i = philox_node<KIND>(w[0], N);
