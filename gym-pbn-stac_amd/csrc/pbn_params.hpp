@@ -149,7 +149,8 @@ struct SSDArgs {
     uint32_t off_planes, off_gap, off_tbit, off_targets, off_hist, lds_bytes;
     int32_t wave;              // 1: one wave per env (k_ssd_wave), small batches
     int32_t dag;               // wave mode: resolve each 64-iteration chunk in parallel (predictor mix,
-                               // or truth tables with <= SSD_DAG_KMAX inputs per node)
+                               // or truth tables with <= SSD_DAG_KMAX inputs per node); the value is
+                               // the waves per env (1, or 4: the workgroup shares one env)
 };
 
 struct SyncArgs {

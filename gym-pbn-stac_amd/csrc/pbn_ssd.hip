@@ -166,7 +166,6 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         constexpr int KOP = KIND == KIND_PREDICTOR_MIX ? 4 : SSD_DAG_KMAX;
         uint32_t* fm = reinterpret_cast<uint32_t*>(wb);                                   // [64][17] flips / P
         unsigned long long* wm = reinterpret_cast<unsigned long long*>(wb + 64 * 17 * 4);  // [512] writers
-        uint32_t* row = reinterpret_cast<uint32_t*>(wb + 64 * 17 * 4 + 512 * 8);          // [16] base state
         auto xor_scan = [lane](uint32_t v) {  // inclusive prefix XOR over the wave's lanes
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -181,15 +180,33 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         uint32_t tg[12];             // target nodes, wave-uniform
 #pragma unroll
         for (int j = 0; j < 12; ++j) tg[j] = j < nt ? uni(targets[j]) : 0u;
-        for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
+        // a.dag == 1: one wave per env (4 envs per workgroup). a.dag == 4: the workgroup's 4 waves
+        // share one env -- each draws and prepares its own chunk (iterations t0 + 64 w ..), then
+        // they resolve in order, wave w once wave w - 1 has written the state row: the state-free
+        // three quarters of the work run on four SIMDs at once.
+        const uint32_t wpe = (uint32_t)a.dag;                      // waves per env
+        // the env's state row (2W dwords): the tail of its first wave's area
+        uint32_t* srow = reinterpret_cast<uint32_t*>(lds + a.off_planes + (wpe == 1 ? wv : 0u) * SSD_WAVE_BYTES +
+                                                     64 * 17 * 4 + 512 * 8);
+        const uint32_t my_turn = wpe == 1 ? 0u : wv;               // resolve order within the env
+        const uint64_t env_stride = wpe == 1 ? waves : (uint64_t)gridDim.x;
+        auto env_sync = [&] {
+            if (wpe == 1)
+                wave_sync();
+            else
+                __syncthreads();
+        };
+        for (uint64_t e = wpe == 1 ? (uint64_t)blockIdx.x * (BLOCK / 64) + wv : (uint64_t)blockIdx.x;; e += env_stride) {
+            if (e >= a.B) break;  // shared mode: e is the same in all four waves (barriers inside)
             const uint64_t g = a.env_base + e;
-            uint32_t rowv = lane < 2u * W ? reinterpret_cast<const uint32_t*>(a.state + e * W)[lane] : 0u;
-            for (uint32_t t0 = 0; t0 < a.iters; t0 += 64) {
-                const uint32_t n = min(64u, a.iters - t0);
+            if (lane < 2u * W && (wpe == 1 || wv == 0)) srow[lane] = reinterpret_cast<const uint32_t*>(a.state + e * W)[lane];
+            env_sync();
+            for (uint32_t t00 = 0; t00 < a.iters; t00 += 64u * wpe) {
+                const uint32_t t0 = t00 + 64u * (wpe == 1 ? 0u : wv);  // this wave's chunk
+                const uint32_t n = t0 < a.iters ? min(64u, a.iters - t0) : 0u;
                 const bool live = lane < n;
                 uint32_t* fmr = fm + lane * 17u;  // own row, stride 17 dwords: conflict-free
                 for (uint32_t k = lane; k < N; k += 64) wm[k] = 0ull;
-                if (lane < 2u * W) row[lane] = rowv;
 #pragma unroll
                 for (int q = 0; q < 2 * W; ++q) fmr[q] = 0u;
                 // ---- draws of iteration t0 + lane (same counters as k_ssd)
@@ -241,58 +258,73 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                 for (int q = 0; q < 2 * W; ++q) fmr[q] = xor_scan(fmr[q]);
                 if (live) atomicOr(&wm[i], 1ull << lane);
                 wave_sync();
-                // ---- operands: last earlier writer (or the initial bit) and the P_c correction
-                uint32_t lw[KOP], has[KOP], cst[KOP];
+                // ---- operands: last earlier writer and the P_c correction (state-free)
+                uint32_t lw[KOP], has[KOP], pcs[KOP];
 #pragma unroll
                 for (int k = 0; k < KOP; ++k) {
                     const unsigned long long m = wm[nd[k]] & below;
                     has[k] = m != 0ull;
                     lw[k] = m ? 63u - (uint32_t)__clzll(m) : 0u;
-                    const uint32_t pc = (fmr[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
-                    const uint32_t init = (row[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
-                    cst[k] = (has[k] ? 0u : init) ^ pc;
+                    pcs[k] = (fmr[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
                 }
                 const uint32_t pself = (fmr[i >> 5] >> (i & 31u)) & 1u;
-                // ---- fixed point over the chunk's updates
-                unsigned long long B = 0ull;  // bit c: base bit stored by update c
-                for (uint32_t r = 0; r <= n; ++r) {
-                    uint32_t x = 0;
+                const uint32_t p_b = tbits(fmr) ^ own_b;  // targets' flips before iteration c
+                const bool last_w = live && (wm[i] >> lane) == 1ull;
+                unsigned long long tw[12];  // writer masks of the targets, below this lane
 #pragma unroll
-                    for (int k = 0; k < KOP; ++k)
-                        if (KIND == KIND_PREDICTOR_MIX || (uint32_t)k < nk)
-                            x = (x << 1) | ((((uint32_t)(B >> lw[k]) & has[k]) ^ cst[k]) & 1u);
-                    const uint32_t yb = ((uint32_t)(ytab >> x) ^ pself) & 1u;
-                    const unsigned long long Bn = __ballot(live && yb);
-                    if (Bn == B) break;
-                    B = Bn;
-                }
-                // ---- histogram: the bucket before iteration c's flips = base ^ P_{c-1} on the targets
-                if (live) {
-                    uint32_t bb = 0;
+                for (int j = 0; j < 12; ++j) tw[j] = j < nt ? wm[tg[j]] & below : 0ull;
+                // ---- resolve, in chunk order across the env's waves
+                for (uint32_t turn = 0; turn < wpe; ++turn) {
+                    if (turn > 0) env_sync();
+                    if (turn != my_turn || n == 0) continue;
+                    uint32_t cst[KOP];
 #pragma unroll
-                    for (int j = 0; j < 12; ++j)
-                        if (j < nt) {
-                            const uint32_t t = tg[j];
-                            const unsigned long long m = wm[t] & below;
-                            const uint32_t v = m ? (uint32_t)(B >> (63u - (uint32_t)__clzll(m))) & 1u
-                                                 : (row[t >> 5] >> (t & 31u)) & 1u;
-                            bb = (bb << 1) | v;
-                        }
-                    atomicAdd(&hist[bb ^ tbits(fmr) ^ own_b], 1u);
+                    for (int k = 0; k < KOP; ++k) {
+                        const uint32_t init = (srow[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
+                        cst[k] = (has[k] ? 0u : init) ^ pcs[k];
+                    }
+                    // ---- fixed point over the chunk's updates
+                    unsigned long long B = 0ull;  // bit c: base bit stored by update c
+                    for (uint32_t r = 0; r <= n; ++r) {
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int k = 0; k < KOP; ++k)
+                            if (KIND == KIND_PREDICTOR_MIX || (uint32_t)k < nk)
+                                x = (x << 1) | ((((uint32_t)(B >> lw[k]) & has[k]) ^ cst[k]) & 1u);
+                        const uint32_t yb = ((uint32_t)(ytab >> x) ^ pself) & 1u;
+                        const unsigned long long Bn = __ballot(live && yb);
+                        if (Bn == B) break;
+                        B = Bn;
+                    }
+                    // ---- histogram: the bucket before iteration c's flips = base ^ P_{c-1} on the targets
+                    if (live) {
+                        uint32_t bb = 0;
+#pragma unroll
+                        for (int j = 0; j < 12; ++j)
+                            if (j < nt) {
+                                const uint32_t t = tg[j];
+                                const uint32_t v = tw[j] ? (uint32_t)(B >> (63u - (uint32_t)__clzll(tw[j]))) & 1u
+                                                         : (srow[t >> 5] >> (t & 31u)) & 1u;
+                                bb = (bb << 1) | v;
+                            }
+                        atomicAdd(&hist[bb ^ p_b], 1u);
+                    }
+                    wave_sync();  // every lane's row reads before the row is rewritten
+                    // ---- the last writer of each node stores its base bit; then base ^ P_{n-1}
+                    if (last_w) {
+                        const uint32_t bit = 1u << (i & 31u);
+                        if ((B >> lane) & 1ull)
+                            atomicOr(&srow[i >> 5], bit);
+                        else
+                            atomicAnd(&srow[i >> 5], ~bit);
+                    }
+                    wave_sync();
+                    if (lane < 2u * W) srow[lane] ^= fm[(n - 1) * 17u + lane];
                 }
-                // ---- the last writer of each node stores its base bit; then base ^ P_{n-1}
-                if (live && (wm[i] >> lane) == 1ull) {
-                    const uint32_t bit = 1u << (i & 31u);
-                    if ((B >> lane) & 1ull)
-                        atomicOr(&row[i >> 5], bit);
-                    else
-                        atomicAnd(&row[i >> 5], ~bit);
-                }
-                wave_sync();
-                rowv = lane < 2u * W ? row[lane] ^ fm[(n - 1) * 17u + lane] : 0u;
-                wave_sync();  // rows and tables are rewritten by the next chunk
+                env_sync();  // the state row is final for this round; tables are rewritten next
             }
-            if (lane < 2u * W) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = rowv;
+            if (lane < 2u * W && (wpe == 1 || wv == 0)) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = srow[lane];
+            env_sync();  // the row is reloaded for the next env
         }
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nb; k += BLOCK)

@@ -125,7 +125,7 @@ void pbn_net_destroy(pbn_net *net);
 /* ---- batches of independent envs (the reference holds one Graph per env) ---- */
 /* Tuning knobs, read from the environment once here (measurement and tests only):
  * PBNSIM_STORE_MODE, PBNSIM_ENVS_PER_THREAD, PBNSIM_STEP_BLOCK (step kernel);
- * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
+ * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL, PBNSIM_SSD_SHARED (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
  * PBNSIM_STEP_GRAPH=0 (pbn_step without HIP graphs). */
 int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
                      pbn_batch **out);
