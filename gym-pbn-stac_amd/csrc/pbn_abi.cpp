@@ -917,6 +917,8 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     a.gap_thr = flip_gap_thr ? d_gap : nullptr;
     a.gap_inv_log2 = flip_gap_thr ? gap_inv_log2(flip_gap_thr, b->N) : 0.0f;
     a.hist = (uint64_t*)b->s_ssd_hist.p;
+    a.error = b->d_error;
+    HIP_TRY(hipMemsetAsync(b->d_error, 0, 4, b->stream));
     // one wave per env while the batch is small against the chip (the reference's 300 resets)
     a.wave = b->ssd_wave >= 0 ? b->ssd_wave : (b->B <= (uint64_t)b->n_cu * 16u ? 1 : 0);
     a.dag = a.wave && !b->ssd_serial && (b->net->kind == PBN_KIND_PREDICTOR_MIX || b->net->kmax <= SSD_DAG_KMAX) ? 1 : 0;
@@ -933,8 +935,11 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     if (e) return fail(PBN_E_HIP, "k_ssd launch: %s", hipGetErrorString((hipError_t)e));
     if (int rc = b->ev_end(stop)) return rc;
     std::vector<uint64_t> h(nb);
+    int32_t err = 0;
     HIP_TRY(hipMemcpyAsync(h.data(), b->s_ssd_hist.p, 8 * nb, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemcpyAsync(&err, b->d_error, 4, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    if (err) return fail(PBN_E_HIP, "k_ssd_wave: a wave timed out waiting for its turn (internal error)");
     for (size_t k = 0; k < nb; k++) hist[k] += h[k];
     b->ssd_iters += iters;
     return 0;

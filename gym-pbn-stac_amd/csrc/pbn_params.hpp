@@ -151,6 +151,7 @@ struct SSDArgs {
     int32_t dag;               // wave mode: resolve each 64-iteration chunk in parallel (predictor mix,
                                // or truth tables with <= SSD_DAG_KMAX inputs per node); the value is
                                // the waves per env (1, or 4: the workgroup shares one env)
+    int32_t* error;            // set to 1 if a shared-mode wave gave up waiting for its turn (never expected)
 };
 
 struct SyncArgs {

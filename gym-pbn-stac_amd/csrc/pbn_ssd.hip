@@ -183,12 +183,14 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         // a.dag == 1: one wave per env (4 envs per workgroup). a.dag == 4: the workgroup's 4 waves
         // share one env -- each draws and prepares its own chunk (iterations t0 + 64 w ..), then
         // they resolve in order, wave w once wave w - 1 has written the state row: the state-free
-        // three quarters of the work run on four SIMDs at once.
+        // three quarters of the work run on four SIMDs at once. The order is a turn counter in
+        // LDS (release / acquire at workgroup scope), not a barrier: a wave that has resolved
+        // its chunk goes on drawing its next one while the later waves resolve theirs.
         const uint32_t wpe = (uint32_t)a.dag;                      // waves per env
         // the env's state row (2W dwords): the tail of its first wave's area
         uint32_t* srow = reinterpret_cast<uint32_t*>(lds + a.off_planes + (wpe == 1 ? wv : 0u) * SSD_WAVE_BYTES +
                                                      64 * 17 * 4 + 512 * 8);
-        const uint32_t my_turn = wpe == 1 ? 0u : wv;               // resolve order within the env
+        uint32_t* turnp = reinterpret_cast<uint32_t*>(lds + a.off_planes + SSD_WAVE_BYTES + 64 * 17 * 4 + 512 * 8);
         const uint64_t env_stride = wpe == 1 ? waves : (uint64_t)gridDim.x;
         auto env_sync = [&] {
             if (wpe == 1)
@@ -200,8 +202,10 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
             if (e >= a.B) break;  // shared mode: e is the same in all four waves (barriers inside)
             const uint64_t g = a.env_base + e;
             if (lane < 2u * W && (wpe == 1 || wv == 0)) srow[lane] = reinterpret_cast<const uint32_t*>(a.state + e * W)[lane];
+            if (wpe > 1 && threadIdx.x == 0) *turnp = 0u;
             env_sync();
-            for (uint32_t t00 = 0; t00 < a.iters; t00 += 64u * wpe) {
+            uint32_t round = 0;
+            for (uint32_t t00 = 0; t00 < a.iters; t00 += 64u * wpe, ++round) {
                 const uint32_t t0 = t00 + 64u * (wpe == 1 ? 0u : wv);  // this wave's chunk
                 const uint32_t n = t0 < a.iters ? min(64u, a.iters - t0) : 0u;
                 const bool live = lane < n;
@@ -274,9 +278,17 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
 #pragma unroll
                 for (int j = 0; j < 12; ++j) tw[j] = j < nt ? wm[tg[j]] & below : 0ull;
                 // ---- resolve, in chunk order across the env's waves
-                for (uint32_t turn = 0; turn < wpe; ++turn) {
-                    if (turn > 0) env_sync();
-                    if (turn != my_turn || n == 0) continue;
+                const uint32_t want = round * wpe + (wpe == 1 ? 0u : wv);
+                if (wpe > 1) {
+                    // the waves of a workgroup are co-resident and wave w - 1 never waits on wave w,
+                    // so the turn always comes; the bound only guards against a logic error
+                    uint32_t spins = 0;
+                    while (__hip_atomic_load(turnp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want &&
+                           ++spins < (1u << 24))
+                        __builtin_amdgcn_s_sleep(1);
+                    if (spins >= (1u << 24) && lane == 0) atomicOr(a.error, 1);
+                }
+                if (n) {
                     uint32_t cst[KOP];
 #pragma unroll
                     for (int k = 0; k < KOP; ++k) {
@@ -321,8 +333,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                     wave_sync();
                     if (lane < 2u * W) srow[lane] ^= fm[(n - 1) * 17u + lane];
                 }
-                env_sync();  // the state row is final for this round; tables are rewritten next
+                wave_sync();  // own tables are rewritten by the next round's draws
+                if (wpe > 1 && lane == 0)  // the next chunk's wave may go (its LDS reads see this chunk's writes)
+                    __hip_atomic_store(turnp, want + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+            env_sync();  // every chunk of the env resolved
             if (lane < 2u * W && (wpe == 1 || wv == 0)) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = srow[lane];
             env_sync();  // the row is reloaded for the next env
         }
