@@ -919,11 +919,14 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     a.hist = (uint64_t*)b->s_ssd_hist.p;
     a.error = b->d_error;
     HIP_TRY(hipMemsetAsync(b->d_error, 0, 4, b->stream));
-    // one wave per env while the batch is small against the chip (the reference's 300 resets)
-    a.wave = b->ssd_wave >= 0 ? b->ssd_wave : (b->B <= (uint64_t)b->n_cu * 16u ? 1 : 0);
+    // one wave per env while the batch is small against the chip (the reference's 300 resets).
+    // Crossovers measured on MI355X (tools/ssd_mode_sweep.py, Bittner-200, p = 0.01, G transitions/s):
+    // 4,096 envs shared 19.4 / wave 16.4 / lane 0.9; 16,384: 18.4 / 19.8 / 3.8; 65,536: - / 20.1 / 14.7;
+    // 262,144: - / 19.8 / 39.4
+    a.wave = b->ssd_wave >= 0 ? b->ssd_wave : (b->B <= (uint64_t)b->n_cu * 256u ? 1 : 0);
     a.dag = a.wave && !b->ssd_serial && (b->net->kind == PBN_KIND_PREDICTOR_MIX || b->net->kmax <= SSD_DAG_KMAX) ? 1 : 0;
     // chunk resolution with the workgroup's 4 waves on one env while even that leaves SIMDs free
-    if (a.dag && (b->ssd_shared >= 0 ? b->ssd_shared == 1 : b->B <= (uint64_t)b->n_cu * 4u)) a.dag = BLOCK / 64;
+    if (a.dag && (b->ssd_shared >= 0 ? b->ssd_shared == 1 : b->B <= (uint64_t)b->n_cu * 16u)) a.dag = BLOCK / 64;
     a.lds_bytes = ssd_layout(b->W, b->net->L.bytes, b->N, n_targets, &a);
     if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "SSD LDS footprint %u B too large", a.lds_bytes);
     hipEvent_t stop;
