@@ -45,7 +45,9 @@ GPU_CASES = [("bittner28", [0, 1, 2, 3, 6, 7, 9], 3000, 0.01), ("bittner199", [0
              ("syn5", [0, 2, 4], 700, 0.05),  # 5 nodes: long in-chunk dependency chains (wave mode rounds)
              ("syn500", [7, 300, 499], 600, 0.01),  # W = 8
              ("tt8", [1, 3, 7], 900, 0.05),  # 8 nodes, 3 inputs each
-             ("ttk7_40", [0, 5, 39], 700, 0.02)]  # 7 inputs per node: past the chunk DAG's 6 (serial apply)
+             ("ttk7_40", [0, 5, 39], 700, 0.02),  # 7 inputs per node: past the chunk DAG's 6 (serial apply)
+             ("bittner199", list(range(0, 120, 10)), 650, 0.02),  # 12 targets: the most the host takes
+             ("bittner28", [4, 5], 10, 0.05)]  # fewer iterations than one chunk
 
 
 def _net(name):
