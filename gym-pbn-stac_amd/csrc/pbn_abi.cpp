@@ -730,7 +730,10 @@ int pbn_step(pbn_batch* b, uint32_t n_updates) {
     CHECK_NN(b, "batch");
     SET_DEV(b);
     uint32_t t = 0;
-    if (n_updates >= STEP_GRAPH_K && b->timing != 1 && step_graph_ready(b)) {
+    // not while the caller is capturing the stream into a graph of its own: plain launches then
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (b->stream && hipStreamIsCapturing(b->stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
+    if (n_updates >= STEP_GRAPH_K && b->timing != 1 && cap == hipStreamCaptureStatusNone && step_graph_ready(b)) {
         // device counter <- update_count (two 32-bit memsets: stream-ordered, no host buffer)
         uint32_t* c = (uint32_t*)b->s_ubase.p;
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c, (int)(uint32_t)b->update_count, 1, b->stream));

@@ -99,6 +99,34 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
     b.close()
 
 
+def test_step_inside_a_torch_graph_capture(G, oracle_mod):
+    """pbn_step on a stream the caller is capturing (torch.cuda.graph) launches plainly into the
+    caller's graph instead of capturing one of its own; replaying the caller's graph repeats the
+    captured launches (same update counters), as any captured launch does."""
+    import torch
+
+    net = load_network("bittner199")
+    o = oracle_mod.Oracle(net)
+    b = G.PBNBatch(net, 3000, seed=5, env_id_base=1)
+    b.randomize()
+    init = b.get_state()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        b.set_stream(s.cuda_stream)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            b.step(70)  # >= 64: would use the batch's own graph outside a capture
+        s.synchronize()
+        b.set_stream(None)
+    assert np.array_equal(b.get_state(), init)  # captured, not run
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(b.get_state(), o.step_philox(init, 5, 1, 0, 70))
+    b.step(1)  # the host counter moved on by 70 during the capture
+    assert np.array_equal(b.get_state(), o.step_philox(init, 5, 1, 0, 71))
+    b.close()
+
+
 @pytest.mark.parametrize("group", ["2", "4", "8"])
 @pytest.mark.parametrize("name", ["bittner28", "bittner199", "syn5", "tt200"])
 def test_rollout_group_mode_matches_oracle(G, oracle_mod, monkeypatch, group, name):
