@@ -190,6 +190,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         // the env's state row (2W dwords): the tail of its first wave's area
         uint32_t* srow = reinterpret_cast<uint32_t*>(lds + a.off_planes + (wpe == 1 ? wv : 0u) * SSD_WAVE_BYTES +
                                                      64 * 17 * 4 + 512 * 8);
+        // shared mode's turn counter: the (otherwise unused) row slot of wave 1's area
         uint32_t* turnp = reinterpret_cast<uint32_t*>(lds + a.off_planes + SSD_WAVE_BYTES + 64 * 17 * 4 + 512 * 8);
         const uint64_t env_stride = wpe == 1 ? waves : (uint64_t)gridDim.x;
         auto env_sync = [&] {
