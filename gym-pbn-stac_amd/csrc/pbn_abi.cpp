@@ -166,6 +166,7 @@ struct pbn_batch {
     hipGraphExec_t step_graph = nullptr;  // STEP_GRAPH_K step launches + k_bump, captured once
     bool step_graph_broken = false;       // capture or instantiation failed once: plain launches
     DevBuf s_ubase;                       // device copy of update_count for graph replays
+    DevBuf s_flip_err;                    // range-error flag of pbn_flip_device
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
@@ -481,7 +482,7 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
-                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase})
+                      &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase, &b->s_flip_err})
         d->release();
     if (b->step_graph) (void)hipGraphExecDestroy(b->step_graph);
     b->pin.release();
@@ -661,6 +662,32 @@ int pbn_flip(pbn_batch* b, const int32_t* actions, int A, int offset, int dedup)
     int e = launch_flip(b->W, a, b->grid_all(b->B), b->stream);
     if (e) return fail(PBN_E_HIP, "k_flip launch: %s", hipGetErrorString((hipError_t)e));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_flip_device(pbn_batch* b, const int32_t* d_actions, int A, int offset, int dedup, int check) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(d_actions, "d_actions");
+    if (A < 1 || A > 4096) return fail(PBN_E_INVALID, "A=%d outside [1, 4096]", A);
+    if (offset != 0 && offset != 1) return fail(PBN_E_INVALID, "offset must be 0 or 1");
+    SET_DEV(b);
+    int32_t* flag = (int32_t*)b->s_flip_err.p;  // zeroed at allocation and after every check
+    if (!flag) {
+        if (int rc = b->s_flip_err.ensure(4)) return rc;
+        flag = (int32_t*)b->s_flip_err.p;
+        HIP_TRY(hipMemsetAsync(flag, 0, 4, b->stream));
+    }
+    FlipArgs a{b->d_state, d_actions, b->B, A, offset, dedup ? 1 : 0, b->N, flag};
+    int e = launch_flip(b->W, a, b->grid_all(b->B), b->stream);
+    if (e) return fail(PBN_E_HIP, "k_flip launch: %s", hipGetErrorString((hipError_t)e));
+    if (!check) return 0;
+    if (!b->pin.ready()) return fail(PBN_E_NOMEM, "pinned staging buffer");
+    HIP_TRY(hipMemcpyAsync(b->pin.p, flag, 4, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemsetAsync(flag, 0, 4, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    int32_t err;
+    memcpy(&err, b->pin.p, 4);
+    if (err) return fail(PBN_E_RANGE, "Invalid action: a value names no node (rows holding one were left untouched)");
     return 0;
 }
 

@@ -268,6 +268,12 @@ class PBNBatch:
         a = np.ascontiguousarray(actions, dtype=np.int32).reshape(self.n_envs, -1)
         L.check(L.lib.pbn_flip(self._h, L.ptr(a, L._i32p), a.shape[1], int(offset), int(bool(dedup))))
 
+    def flip_device(self, d_actions: int, A: int, offset: int = 1, dedup: bool = True, check: bool = True):
+        """``flip`` with device actions (``d_actions``: pointer to int32 ``[B][A]`` on this GPU).
+        ``check=False`` returns at once; range errors are then raised by the next checked call."""
+        L.check(L.lib.pbn_flip_device(self._h, C.c_void_p(int(d_actions)), int(A), int(offset), int(bool(dedup)),
+                                      int(bool(check))))
+
     def step(self, n_updates: int = 1):
         L.check(L.lib.pbn_step(self._h, int(n_updates)))
 

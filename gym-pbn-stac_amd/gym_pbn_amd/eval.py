@@ -70,19 +70,69 @@ def ssd_counts_controlled(network, target_nodes: Sequence[int], iters: int, rese
     return counts
 
 
+def ssd_counts_controlled_device(network, target_nodes: Sequence[int], iters: int, resets: int, policy,
+                                 seed: int = 0, device: int = 0, initial_states: Optional[np.ndarray] = None):
+    """``ssd_counts_controlled`` with the whole loop on the GPU: ``policy`` is a torch callable
+    taking the observations as a uint8 tensor ``[resets][N]`` on the device and returning the
+    actions (node + 1, 0 = none) as an integer tensor ``[resets]`` or ``[resets][A]`` there. Per
+    iteration (eval.py:84-101): bucket counted on the device, ``policy`` called once for every
+    reset, flip (``pbn_flip_device``), one transition -- everything on torch's current stream,
+    no observation or action crosses PCIe. Same counts as ``ssd_counts_controlled`` with a
+    ``model.predict`` computing the same actions."""
+    import torch
+
+    b = PBNBatch(network, resets, device=device, seed=seed)
+    if initial_states is None:
+        b.randomize()
+    else:
+        b.set_state(initial_states)
+    dev = torch.device("cuda", device)
+    b.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    try:
+        N = b.n_nodes
+        t = torch.as_tensor(np.asarray(target_nodes, dtype=np.int64), device=dev)
+        g = t.numel()
+        weights = (2.0 ** torch.arange(g - 1, -1, -1, device=dev)).float()  # first target = MSB; exact (g <= 12)
+        span = min(iters, 256)  # iterations whose buckets are counted together
+        buckets = torch.empty((span, resets), dtype=torch.int16, device=dev)
+        counts = torch.zeros(1 << g, dtype=torch.int64, device=dev)
+        obs = torch.empty((resets, N), dtype=torch.uint8, device=dev)
+        for k in range(iters):
+            b.unpack_bits_device(obs.data_ptr())
+            buckets[k % span] = obs[:, t].float().matmul(weights).to(torch.int16)
+            if k % span == span - 1 or k == iters - 1:
+                counts += torch.bincount(buckets[:k % span + 1].reshape(-1).long(), minlength=1 << g)
+            act = torch.as_tensor(policy(obs), device=dev)
+            act = act.reshape(resets, -1).to(torch.int32).contiguous()
+            # range errors surface at the last iteration's checked call (the reference would
+            # raise at the first; rows with a bad action are left untouched either way)
+            b.flip_device(act.data_ptr(), act.shape[1], offset=1, dedup=True, check=k == iters - 1)
+            b.step(1)
+        out = counts.cpu().numpy().astype(np.uint64)
+    finally:
+        torch.cuda.current_stream(dev).synchronize()
+        b.set_stream(None)
+        b.close()
+    return out
+
+
 def compute_ssd_hist(network, target_nodes: Sequence[int], iters: int = 1_200_000, resets: int = 300,
                      bit_flip_prob: float = 0.01, seed: int = 0, device: int = 0,
-                     initial_states: Optional[np.ndarray] = None, model=None):
+                     initial_states: Optional[np.ndarray] = None, model=None, policy=None):
     """Normalised SSD histogram as a DataFrame indexed by the bucket bit strings (eval.py:62-69).
 
     ``model`` given: the controlled SSD (actions from ``model.predict``, no bit-flip noise,
-    eval.py:96-101); otherwise the uncontrolled run with Bernoulli bit flips, all on the device."""
+    eval.py:96-101); ``policy`` given: the same with a torch policy on the device
+    (``ssd_counts_controlled_device``); otherwise the uncontrolled run with Bernoulli bit flips,
+    all on the device."""
     assert 0 <= bit_flip_prob <= 1, "Invalid Bit Flip Probability value."  # eval.py:32-34
     assert resets > 0, "Invalid resets value."
     assert iters > 0, "Invalid iterations value."
     assert iters // resets, "Resets does not divide the iterations."
     per = iters // resets
-    if model is None:
+    if policy is not None:
+        counts = ssd_counts_controlled_device(network, target_nodes, per, resets, policy, seed, device, initial_states)
+    elif model is None:
         counts = ssd_counts(network, target_nodes, per, resets, bit_flip_prob, seed, device, initial_states)
     else:
         counts = ssd_counts_controlled(network, target_nodes, per, resets, model, seed, device, initial_states)

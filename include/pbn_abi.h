@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 7
+#define PBN_ABI_VERSION 8
 
 enum {
     PBN_OK = 0,
@@ -153,6 +153,12 @@ int pbn_randomize_state(pbn_batch *b);
  * (offset 1: gym-PBN target envs, pbn_target.py:266-267; offset 0: PBNEnv, pbn_env.py:141-142).
  * dedup 1: act on unique values per row (torch-tensor input, pbn_target_multi.py:120-121). */
 int pbn_flip(pbn_batch *b, const int32_t *actions, int A, int offset, int dedup);
+/* Same with the actions already on the device (d_actions [B][A] int32, e.g. a torch policy's
+ * output), on the batch stream. A row holding an out-of-range value is left untouched (the other
+ * rows are flipped) and noted in a device flag. check 1: wait for the kernel, return PBN_E_RANGE
+ * if the flag is set (by this call or by earlier check-0 calls) and clear it; check 0: return
+ * at once (asynchronous; a later check-1 call reports). */
+int pbn_flip_device(pbn_batch *b, const int32_t *d_actions, int A, int offset, int dedup, int check);
 
 /* ---- the hot path: Graph.step (base.py:306-312) / PBN.step (pbn.py:129-133) ---- */
 /* Philox mode, n_updates launches of one update each (state round-trips HBM). Runs of 64

@@ -140,3 +140,45 @@ def test_controlled_ssd_matches_stepwise_oracle(oracle_mod):
     assert abs(df["Value"].sum() - 1.0) < 1e-9
     inc = eval_increase(net, targets, _RulePolicy(), [(0,) * 7, (1,) * 7], iters=iters * B, resets=B, seed=11)
     assert np.isfinite(inc)
+
+
+@pytest.mark.gpu
+def test_controlled_ssd_device_policy_matches_host_model():
+    """The device-resident controlled SSD (torch policy on the GPU, pbn_flip_device) gives the
+    same counts as the host path with an SB3-style model.predict computing the same actions;
+    an out-of-range device action raises ValueError and leaves its row untouched."""
+    import torch
+
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.eval import ssd_counts_controlled, ssd_counts_controlled_device
+
+    net = load_network("bittner28")
+    N = net.n_nodes
+
+    class Model:
+        def predict(self, obs, target, deterministic=True):
+            return (obs[:, :6].astype(np.int64) * np.arange(1, 7)).sum(1) % (N + 1), None
+
+    def policy(obs):
+        return (obs[:, :6].long() * torch.arange(1, 7, device=obs.device)).sum(1) % (N + 1)
+
+    targets = [0, 1, 2, 3, 6, 7, 9]
+    host = ssd_counts_controlled(net, targets, 300, 64, Model(), seed=11)
+    dev = ssd_counts_controlled_device(net, targets, 300, 64, policy, seed=11)
+    assert np.array_equal(host, dev) and int(dev.sum()) == 300 * 64
+
+    b = PBNBatch(net, 4, seed=2)
+    b.randomize()
+    s0 = b.get_state()
+    acts = torch.tensor([[1, 0], [N + 1, 0], [3, 3], [0, 0]], dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        b.flip_device(acts.data_ptr(), 2)
+    s1 = b.get_state()
+    assert s1[1] == s0[1] and s1[3] == s0[3]  # the bad row and the no-op row
+    assert s1[0] == s0[0] ^ np.uint64(1) and s1[2] == s0[2] ^ np.uint64(1 << 2)  # dedup: [3, 3] flips once
+    b.flip_device(acts.data_ptr(), 2, check=False)  # asynchronous: the error waits for a checked call
+    ok = torch.zeros((4, 1), dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        b.flip_device(ok.data_ptr(), 1)
+    b.flip_device(ok.data_ptr(), 1)  # the flag was cleared by the check
+    b.close()
