@@ -146,12 +146,14 @@ def compute_ssd_hist(network, target_nodes: Sequence[int], iters: int = 1_200_00
 
 def eval_increase(network, target_nodes: Sequence[int], model, target_node_values, original_ssd=None,
                   iters: int = 1_200_000, resets: int = 300, bit_flip_prob: float = 0.01, seed: int = 0,
-                  device: int = 0) -> float:
+                  device: int = 0, policy=None) -> float:
     """Total increase of the favourable buckets between the uncontrolled and the controlled
     SSD (``eval_increase``, eval.py:106-136). ``target_node_values`` are the favourable
-    target-node value tuples (the reference's ``env.target_node_values``)."""
+    target-node value tuples (the reference's ``env.target_node_values``). ``policy`` (a torch
+    policy on the device) replaces ``model`` for the controlled run when given."""
     if original_ssd is None:  # cache, as the reference
         original_ssd = compute_ssd_hist(network, target_nodes, iters, resets, bit_flip_prob, seed, device)
-    model_ssd = compute_ssd_hist(network, target_nodes, iters, resets, bit_flip_prob, seed, device, model=model)
+    model_ssd = compute_ssd_hist(network, target_nodes, iters, resets, bit_flip_prob, seed, device, model=model,
+                                 policy=policy)
     states_of_interest = [_bit_seq_to_str(s) for s in target_node_values]
     return float((model_ssd - original_ssd).loc[states_of_interest, "Value"].sum())
