@@ -176,6 +176,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         };
         const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
         auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+        auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
         const int nt = a.n_targets;  // <= 12 (host check)
         uint32_t tg[12];             // target nodes, wave-uniform
 #pragma unroll
@@ -289,6 +290,8 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                         __builtin_amdgcn_s_sleep(1);
                     if (spins >= (1u << 24) && lane == 0) atomicOr(a.error, 1);
                 }
+                unsigned long long B = 0ull;  // bit c: base bit stored by update c
+                uint32_t tinit = 0;           // the targets' bits at the chunk start (first = MSB)
                 if (n) {
                     uint32_t cst[KOP];
 #pragma unroll
@@ -296,8 +299,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                         const uint32_t init = (srow[nd[k] >> 5] >> (nd[k] & 31u)) & 1u;
                         cst[k] = (has[k] ? 0u : init) ^ pcs[k];
                     }
+                    const uint32_t sv = lane < 2u * W ? srow[lane] : 0u;
+#pragma unroll
+                    for (int j = 0; j < 12; ++j)
+                        if (j < nt) tinit = (tinit << 1) | ((rl(sv, tg[j] >> 5) >> (tg[j] & 31u)) & 1u);
                     // ---- fixed point over the chunk's updates
-                    unsigned long long B = 0ull;  // bit c: base bit stored by update c
                     for (uint32_t r = 0; r <= n; ++r) {
                         uint32_t x = 0;
 #pragma unroll
@@ -308,19 +314,6 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                         const unsigned long long Bn = __ballot(live && yb);
                         if (Bn == B) break;
                         B = Bn;
-                    }
-                    // ---- histogram: the bucket before iteration c's flips = base ^ P_{c-1} on the targets
-                    if (live) {
-                        uint32_t bb = 0;
-#pragma unroll
-                        for (int j = 0; j < 12; ++j)
-                            if (j < nt) {
-                                const uint32_t t = tg[j];
-                                const uint32_t v = tw[j] ? (uint32_t)(B >> (63u - (uint32_t)__clzll(tw[j]))) & 1u
-                                                         : (srow[t >> 5] >> (t & 31u)) & 1u;
-                                bb = (bb << 1) | v;
-                            }
-                        atomicAdd(&hist[bb ^ p_b], 1u);
                     }
                     wave_sync();  // every lane's row reads before the row is rewritten
                     // ---- the last writer of each node stores its base bit; then base ^ P_{n-1}
@@ -334,9 +327,23 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
                     wave_sync();
                     if (lane < 2u * W) srow[lane] ^= fm[(n - 1) * 17u + lane];
                 }
-                wave_sync();  // own tables are rewritten by the next round's draws
+                wave_sync();
                 if (wpe > 1 && lane == 0)  // the next chunk's wave may go (its LDS reads see this chunk's writes)
                     __hip_atomic_store(turnp, want + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // ---- histogram, off the chain of resolutions: the bucket before iteration c's flips
+                // = base ^ P_{c-1} on the targets, from the writer masks, B and the chunk-start bits
+                if (live) {
+                    uint32_t bb = 0;
+#pragma unroll
+                    for (int j = 0; j < 12; ++j)
+                        if (j < nt) {
+                            const uint32_t v = tw[j] ? (uint32_t)(B >> (63u - (uint32_t)__clzll(tw[j]))) & 1u
+                                                     : (tinit >> (nt - 1 - j)) & 1u;
+                            bb = (bb << 1) | v;
+                        }
+                    atomicAdd(&hist[bb ^ p_b], 1u);
+                }
+                wave_sync();  // own tables are rewritten by the next round's draws
             }
             env_sync();  // every chunk of the env resolved
             if (lane < 2u * W && (wpe == 1 || wv == 0)) reinterpret_cast<uint32_t*>(a.state + e * W)[lane] = srow[lane];
