@@ -160,7 +160,8 @@ struct pbn_batch {
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
-    int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 1 = four waves per env, 0 = one, -1 = by size
+    int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
+                              // count, -1 = by size
     int roll_group = 1;       // PBNSIM_ROLL_GROUP: lanes per env of the rollout kernel (default by size)
     bool step_graph_off = false;  // PBNSIM_STEP_GRAPH=0: step mode without HIP graphs
     hipGraphExec_t step_graph = nullptr;  // STEP_GRAPH_K step launches + k_bump, captured once
@@ -438,7 +439,10 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
-    if (const char* v = getenv("PBNSIM_SSD_SHARED")) b->ssd_shared = atoi(v) ? 1 : 0;
+    if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
+        const int w = atoi(v);
+        b->ssd_shared = w == 0 ? 0 : (w == 4 || w == 8) ? w : 1;
+    }
     if (const char* v = getenv("PBNSIM_STEP_GRAPH")) b->step_graph_off = atoi(v) == 0;
     // rollout lanes per env: 1 = k_rollout; 2/4/8 = k_rollout_grp (predictor mix, N <= 256)
     b->roll_group = roll_group_size(b, net);
@@ -956,7 +960,8 @@ int pbn_ssd_run(pbn_batch* b, const int32_t* target_nodes, int n_targets, const 
     a.wave = b->ssd_wave >= 0 ? b->ssd_wave : (b->B <= (uint64_t)b->n_cu * 256u ? 1 : 0);
     a.dag = a.wave && !b->ssd_serial && (b->net->kind == PBN_KIND_PREDICTOR_MIX || b->net->kmax <= SSD_DAG_KMAX) ? 1 : 0;
     // chunk resolution with the workgroup's 4 waves on one env while even that leaves SIMDs free
-    if (a.dag && (b->ssd_shared >= 0 ? b->ssd_shared == 1 : b->B <= (uint64_t)b->n_cu * 16u)) a.dag = BLOCK / 64;
+    if (a.dag && (b->ssd_shared >= 0 ? b->ssd_shared > 0 : b->B <= (uint64_t)b->n_cu * 8u))
+        a.dag = b->ssd_shared > 1 ? b->ssd_shared : SSD_SHARED_WAVES;
     a.lds_bytes = ssd_layout(b->W, b->net->L.bytes, b->N, n_targets, &a);
     if (a.lds_bytes > 160u * 1024u) return fail(PBN_E_UNSUPPORTED, "SSD LDS footprint %u B too large", a.lds_bytes);
     hipEvent_t stop;

@@ -132,7 +132,10 @@ struct MTArgs {
     uint32_t* pos_np;
 };
 
-constexpr int SSD_DAG_KMAX = 6;  // truth-table nodes with more inputs: k_ssd_wave applies serially
+constexpr int SSD_DAG_KMAX = 6;
+// waves per env in shared mode (k_ssd_wave): 4 measured faster than 8 (300 envs x 4,000: 0.19 vs
+// 0.23 ms; 1,024 envs: 10.4 vs 8.8 G transitions/s; tools/ssd_shared_sweep.py)
+constexpr int SSD_SHARED_WAVES = 4;  // truth-table nodes with more inputs: k_ssd_wave applies serially
 
 struct SSDArgs {
     uint64_t* state;           // [B][W]
@@ -184,6 +187,7 @@ constexpr uint32_t ENV_CHUNK = PBN_ENV_CHUNK;  // updates per lane between refil
 constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
+uint32_t ssd_block(const SSDArgs& a);
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a);
 int launch_ssd(int W, const SSDArgs& a, int grid, void* stream);
 uint32_t sync_layout(int W, uint32_t image_bytes, int n_nodes, SyncArgs* a);

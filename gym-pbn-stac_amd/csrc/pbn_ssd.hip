@@ -111,9 +111,11 @@ struct RowT {
 // per wave: LDS-row path 64*8 + 64*8 + 64*2*SSD_FMAX + 64 + 16*8 = 2,752 B; predictor-mix path
 // flips/prefixes [64][17] u32 + writer masks [512] u64 + base row [16] u32 = 8,512 B
 constexpr uint32_t SSD_WAVE_BYTES = 64 * 17 * 4 + 512 * 8 + 16 * 4;
+constexpr uint32_t SSD_WAVE_MAX_BLOCK = 512;  // shared mode: up to 8 waves on one env
 
 template <int W, int KIND>
-__global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
+__global__ __launch_bounds__(SSD_WAVE_MAX_BLOCK) void k_ssd_wave(SSDArgs a) {
+    const uint32_t BLK = blockDim.x;  // 256, or 64 x the waves per env in shared mode
     extern __shared__ __align__(16) uint8_t lds[];
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     const uint32_t N = (uint32_t)a.L.n_nodes;
@@ -122,13 +124,13 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
     int16_t* tbit = reinterpret_cast<int16_t*>(lds + a.off_tbit);
     uint16_t* targets = reinterpret_cast<uint16_t*>(lds + a.off_targets);
     uint32_t* hist = reinterpret_cast<uint32_t*>(lds + a.off_hist);
-    for (uint32_t k = threadIdx.x; k < N; k += BLOCK) {
+    for (uint32_t k = threadIdx.x; k < N; k += BLK) {
         gap[k] = a.gap_thr ? a.gap_thr[k] : 0xFFFFFFFFu;
         tbit[k] = -1;
     }
-    for (uint32_t k = threadIdx.x; k < nb; k += BLOCK) hist[k] = 0;
+    for (uint32_t k = threadIdx.x; k < nb; k += BLK) hist[k] = 0;
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < (uint32_t)a.n_targets; j += BLOCK) {
+    for (uint32_t j = threadIdx.x; j < (uint32_t)a.n_targets; j += BLK) {
         targets[j] = (uint16_t)a.targets[j];
         tbit[a.targets[j]] = (int16_t)(a.n_targets - 1 - (int)j);
     }
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    const uint64_t waves = (uint64_t)gridDim.x * (BLK / 64);
     if (a.dag) {
         // Parallel in time: lane c owns iteration t0 + c of a 64-iteration chunk. All draws
         // (flips, node, predictor record) are independent of the state, so lane c has them before
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
             else
                 __syncthreads();
         };
-        for (uint64_t e = wpe == 1 ? (uint64_t)blockIdx.x * (BLOCK / 64) + wv : (uint64_t)blockIdx.x;; e += env_stride) {
+        for (uint64_t e = wpe == 1 ? (uint64_t)blockIdx.x * (BLK / 64) + wv : (uint64_t)blockIdx.x;; e += env_stride) {
             if (e >= a.B) break;  // shared mode: e is the same in all four waves (barriers inside)
             const uint64_t g = a.env_base + e;
             if (lane < 2u * W && (wpe == 1 || wv == 0)) srow[lane] = reinterpret_cast<const uint32_t*>(a.state + e * W)[lane];
@@ -350,11 +352,11 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
             env_sync();  // the row is reloaded for the next env
         }
         __syncthreads();
-        for (uint32_t k = threadIdx.x; k < nb; k += BLOCK)
+        for (uint32_t k = threadIdx.x; k < nb; k += BLK)
             if (hist[k]) atomicAdd(reinterpret_cast<unsigned long long*>(a.hist) + k, (unsigned long long)hist[k]);
         return;
     }
-    for (uint64_t e = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; e < a.B; e += waves) {
+    for (uint64_t e = (uint64_t)blockIdx.x * (BLK / 64) + wv; e < a.B; e += waves) {
         const uint64_t g = a.env_base + e;
         if (lane < 2u * W) R.put(lane, reinterpret_cast<const uint32_t*>(a.state + e * W)[lane]);
         wave_sync();
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(BLOCK) void k_ssd_wave(SSDArgs a) {
         wave_sync();
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nb; k += BLOCK)
+    for (uint32_t k = threadIdx.x; k < nb; k += BLK)
         if (hist[k]) atomicAdd(reinterpret_cast<unsigned long long*>(a.hist) + k, (unsigned long long)hist[k]);
 }
 
@@ -470,9 +472,12 @@ static void* ssd_fn(int W) {
 
 static uint32_t a16(uint32_t x) { return (x + 15u) & ~15u; }
 
+// threads per workgroup: shared mode puts a.dag waves on one env, every other mode runs 256
+uint32_t ssd_block(const SSDArgs& a) { return a.wave && a.dag > 1 ? 64u * (uint32_t)a.dag : (uint32_t)BLOCK; }
+
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a) {
     a->off_planes = image_bytes;  // lane mode: state planes; wave mode: per-wave chunk buffers + row
-    const uint32_t per_block = a->wave ? (BLOCK / 64) * SSD_WAVE_BYTES : 8u * (uint32_t)W * BLOCK;
+    const uint32_t per_block = a->wave ? ssd_block(*a) / 64u * SSD_WAVE_BYTES : 8u * (uint32_t)W * BLOCK;
     a->off_gap = a16(a->off_planes + per_block);
     a->off_tbit = a16(a->off_gap + 4u * (uint32_t)n_nodes);
     a->off_targets = a16(a->off_tbit + 2u * (uint32_t)n_nodes);
@@ -492,7 +497,7 @@ int launch_ssd(int W, const SSDArgs& a, int grid, void* stream) {
         if (e != hipSuccess) return (int)e;
     }
     void* kargs[] = {&c};
-    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
+    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(ssd_block(a)), kargs, lds, (hipStream_t)stream);
 }
 
 }  // namespace pbn

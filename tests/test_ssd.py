@@ -67,14 +67,14 @@ def _net(name):
 @pytest.mark.gpu
 # one lane per env / one wave per env (chunk resolved in parallel) / four waves per env (chunks
 # prepared in parallel, resolved in order) / one wave per env, serial apply
-@pytest.mark.parametrize("mode", ["lane", "wave", "shared", "wave_serial"])
+@pytest.mark.parametrize("mode", ["lane", "wave", "shared", "shared8", "wave_serial"])
 @pytest.mark.parametrize("name,targets,iters,p", GPU_CASES)
 def test_ssd_matches_oracle(oracle_mod, monkeypatch, mode, name, targets, iters, p):
     from gym_pbn_amd.batch import PBNBatch, flip_gap_table
 
     monkeypatch.setenv("PBNSIM_SSD_WAVE", "0" if mode == "lane" else "1")
     monkeypatch.setenv("PBNSIM_SSD_SERIAL", "1" if mode == "wave_serial" else "0")
-    monkeypatch.setenv("PBNSIM_SSD_SHARED", "1" if mode == "shared" else "0")
+    monkeypatch.setenv("PBNSIM_SSD_SHARED", {"shared": "4", "shared8": "8"}.get(mode, "0"))
     net = _net(name)
     B = 600
     b = PBNBatch(net, B, seed=17, env_id_base=5)
