@@ -152,6 +152,29 @@ def test_rollout_group_mode_matches_oracle(G, oracle_mod, monkeypatch, group, na
         b.close()
 
 
+@pytest.mark.parametrize("case", range(4))
+def test_rollout_random_shapes_all_lane_counts(G, oracle_mod, monkeypatch, case):
+    """Seeded random batch sizes and update counts: rollout with 1, 2, 4 and 8 lanes per env and
+    step mode (plain and graph-replayed launches) all give the oracle's states."""
+    rng = np.random.default_rng(77 + case)
+    net = load_network(["bittner28", "bittner199"][case % 2])
+    o = oracle_mod.Oracle(net)
+    B = int(rng.integers(1, 3000))
+    T = int(rng.integers(2, 200))
+    ref = None
+    for group in ("1", "2", "4", "8"):
+        monkeypatch.setenv("PBNSIM_ROLL_GROUP", group)
+        b = G.PBNBatch(net, B, seed=case, env_id_base=case * 11)
+        b.randomize()
+        init = b.get_state()
+        if ref is None:
+            ref = o.step_philox(init, case, case * 11, 0, 2 * T)
+        b.rollout(T)
+        b.step(T)
+        assert np.array_equal(b.get_state(), ref), (group, B, T)
+        b.close()
+
+
 @pytest.mark.parametrize("name", ["bittner199", "bittner28"])
 def test_ragged_batches_and_zero_updates(G, oracle_mod, name):
     """Batch sizes that fill no wave / workgroup / pair evenly (1, 63, 65, 1023, 1025, 4097, 70001):

@@ -182,3 +182,36 @@ def test_controlled_ssd_device_policy_matches_host_model():
         b.flip_device(ok.data_ptr(), 1)
     b.flip_device(ok.data_ptr(), 1)  # the flag was cleared by the check
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(6))
+def test_ssd_random_shapes_all_modes_agree(oracle_mod, monkeypatch, case):
+    """Seeded random batch sizes, run lengths, flip rates and target sets: every mode (lane,
+    one wave, four and eight waves per env) gives the oracle's counts and states."""
+    from gym_pbn_amd.batch import PBNBatch, flip_gap_table
+
+    rng = np.random.default_rng(1000 + case)
+    name = ["bittner28", "bittner199", "tt200"][case % 3]
+    net = _net(name)
+    B = int(rng.integers(1, 700))
+    iters = int(rng.integers(1, 900))
+    p = float(rng.choice([0.0, 0.005, 0.05]))
+    targets = sorted(rng.choice(net.n_nodes, size=int(rng.integers(1, 9)), replace=False).tolist())
+    rng.shuffle(targets)  # any order: the first target is the most significant bucket bit
+    o = oracle_mod.Oracle(net)
+    gap = flip_gap_table(net.n_nodes, p)
+    ref = None
+    for wave, shared in (("0", "0"), ("1", "0"), ("1", "4"), ("1", "8")):
+        monkeypatch.setenv("PBNSIM_SSD_WAVE", wave)
+        monkeypatch.setenv("PBNSIM_SSD_SHARED", shared)
+        b = PBNBatch(net, B, seed=case, env_id_base=3 * case)
+        b.randomize()
+        s0 = b.get_state()
+        h = b.ssd_counts(targets, iters, p)
+        if ref is None:
+            st, r = oracle_mod.ssd_philox(o, s0, targets, gap, case, 3 * case, 0, iters)
+            ref = (st, r)
+        assert np.array_equal(h, ref[1]), (wave, shared)
+        assert np.array_equal(b.get_state(), ref[0]), (wave, shared)
+        b.close()
