@@ -113,6 +113,28 @@ def beyond_mall_supplement(net, device, seed):
             "achieved_GBs": alg / s / 1e9, "frac": alg / s / 1e9 / HBM_PEAK_GBS}
 
 
+def copy_bandwidth(device, gib: float = 2.0, reps: int = 10):
+    """Achievable HBM rate on this box: a device-to-device copy of a buffer far past the MALL,
+    (read + write bytes) / time from CUDA events. Context for the roofline's fractions."""
+    import torch
+
+    n = int(gib * (1 << 30))
+    src = torch.empty(n, dtype=torch.uint8, device=f"cuda:{device}")
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    t1.record()
+    torch.cuda.synchronize()
+    s = t0.elapsed_time(t1) / 1e3 / reps
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2 * n / s / 1e9
+
+
 def config2_supplement(device):
     """BASELINE config 2 beside the main line: Bittner-28 (predictor_sets_28_15_median, N = 28,
     one state word), 65,536 envs on one GPU (512 KiB of state: launch-bound in step mode), step
@@ -374,6 +396,15 @@ def main():
         except Exception as exc:  # a supplement must not cost the main line
             r6 = {"error": f"{type(exc).__name__}: {exc}"}
     if rank == 0:
+        try:  # achievable-copy rate on this box beside the spec peak
+            copy = copy_bandwidth(device)
+            rf = out["roofline"]
+            rf["achievable_copy_GBs"] = copy
+            rf["achievable_copy_source"] = ("torch device-to-device copy of 2 GiB (past the MALL), read + write "
+                                            "bytes / CUDA-event time; the kernel's traffic_GBs also counts "
+                                            "MALL-served fetches, so it can exceed this")
+        except Exception as exc:  # a supplement must not cost the main line
+            out["roofline"]["achievable_copy_GBs"] = f"error: {type(exc).__name__}: {exc}"
         out["config2_bittner28"] = cfg2
         out["config5_r6"] = r6
         if not args.no_cpu_baseline and world == 1:  # the host-core baseline: rank 0 at N = 1 only
