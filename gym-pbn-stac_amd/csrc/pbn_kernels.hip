@@ -464,6 +464,18 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             uint64_t* gid_tab = reinterpret_cast<uint64_t*>(gw + ENV_CHUNK * 128 + 64 + 256);  // [64]
             uint32_t* call_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64 + 256 + 512);  // [64]
             const uint32_t nact = (uint32_t)__popcll(act);
+            if (nact == 64) {
+                // every lane active: draw k of round sl belongs to lane k itself, so each lane
+                // draws its own entries from its registers (no rank / counter tables)
+                const uint64_t gid = a.env_base + (uint64_t)e;
+                for (uint32_t sl = 0; sl < ENV_CHUNK; ++sl) {
+                    uint32_t w[4];
+                    philox_draw(a.seed, used + sl, a.call_idx + t, gid, STREAM_ENV, w);
+                    const uint32_t i = philox_node<KIND>(w[0], N);
+                    const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
+                    gbuf[sl * 64 + lane] = (uint16_t)(i | (j << 9));
+                }
+            } else {
             if (e >= 0) {
                 lane_of_rank[__popcll(act & ((1ull << lane) - 1ull))] = (uint8_t)lane;
                 used_tab[lane] = used;
@@ -488,6 +500,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                     const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
                     gbuf[sl * 64 + q] = (uint16_t)(i | (j << 9));
                 }
+            }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
