@@ -356,6 +356,8 @@ __device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* c
 
 __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
+constexpr uint32_t ENV_OWN_DRAWS_MIN = 40;  // active lanes from which a wave skips the shared draw tables
+
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     static_assert(FAST != 2 || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
@@ -464,9 +466,11 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             uint64_t* gid_tab = reinterpret_cast<uint64_t*>(gw + ENV_CHUNK * 128 + 64 + 256);  // [64]
             uint32_t* call_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64 + 256 + 512);  // [64]
             const uint32_t nact = (uint32_t)__popcll(act);
-            if (nact == 64) {
-                // every lane active: draw k of round sl belongs to lane k itself, so each lane
-                // draws its own entries from its registers (no rank / counter tables)
+            if (nact >= ENV_OWN_DRAWS_MIN) {
+                // (nearly) every lane active: each lane draws its own entries from its registers
+                // -- no rank / counter tables; an idle lane's draws are junk nobody reads. Fewer
+                // rounds shared over the wave stop paying off below ~40 active lanes (a shared
+                // round costs two dependent LDS round trips more)
                 const uint64_t gid = a.env_base + (uint64_t)e;
                 for (uint32_t sl = 0; sl < ENV_CHUNK; ++sl) {
                     uint32_t w[4];
