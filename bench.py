@@ -6,22 +6,35 @@ batch=1M; achieved HBM GB/s"): the exported ``predictor_sets_200_5_kmeans`` netw
 (N=199 nodes, 994 predictors, W=4 state words), 1,048,576 independent envs per GPU
 resident in HBM as bit-packed uint64 words. One bench *step* = one R1 async
 transition (``Graph.step``, base.py:306-312) for every env = one ``pbn_step`` launch
-(state read from and written back to HBM). Philox4x32-10 RNG in-register.
+(state read from and written back to device memory). Philox4x32-10 RNG in-register.
 
-Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``):
-each rank owns 1,048,576 envs with global ids [rank*B, (rank+1)*B) -- weak scaling,
-no data-path collective (envs are independent); barrier + max-over-ranks timing.
+Multi-GPU: ``python bench.py --gpus N`` starts ``torch.distributed.run`` with N ranks as a
+child process (before anything touches a GPU) when ``WORLD_SIZE`` is not set, and exits with
+its code; under ``torch.distributed.run`` ``--gpus`` must equal ``WORLD_SIZE``. Each rank owns
+1,048,576 envs with global ids [rank*B, (rank+1)*B) -- weak scaling, no data-path collective
+(envs are independent); barrier + max-over-ranks timing; ``n_gpus`` = the process group's size.
 
-Prints ONE JSON line (rank 0) with ``roofline`` (algorithmic bytes / kernel time from
-HIP events on the batch stream) and ``cpu_baseline`` (the oracle's C restatement on
-host cores, rank 0 only).
+Order: the supplementary measurements (rollout, BASELINE config 2, the past-MALL 8M-env
+step run, config 5's R6 chunks with their all-gather) run FIRST, the headline's W warm-up and
+K timed launches after them: at K = 20 the line would otherwise time the GPU's clock ramp
+(9.4 us per launch after 5 warm-up launches, 7.0 us after 5,000). The memory
+floor of the same access pattern (``tools/mall_probe.hip``) is measured right after the timed
+launches, in the same clock state, and is the 1M line's roofline peak (the 32 MiB state stays
+in the Infinity Cache / L2 between launches, and MI355X_MICROARCH.md gives no streaming figure
+for those); the HBM roofline (8 TB/s spec) comes from the 8M-env run (256 MiB of state).
+
+Prints ONE JSON line (rank 0) with ``roofline`` and ``cpu_baseline`` (the oracle's C
+restatement on host cores, rank 0 at N = 1 only).
 """
 
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -30,6 +43,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s
 
 
 def parse():
@@ -42,19 +56,21 @@ def parse():
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--no-events", action="store_true", help="time without per-launch HIP events")
     p.add_argument("--rollout", type=int, default=64, help="updates per launch for the supplementary rollout line")
     p.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    p.add_argument("--valu-file", default=str(ROOT / "profiles" / "r02_valu_pmc.json"))
     p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
     p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
     p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
     p.add_argument("--no-config2", dest="config2", action="store_false", help="skip the Bittner-28 supplement")
-    p.add_argument("--beyond-mall", action="store_true",
-                   help="add the 8M-env (state past the MALL) step-mode supplement (off by default: it launches "
-                        "the bench kernel at another size, which would mix into a rocprof average of the line)")
+    p.add_argument("--no-beyond-mall", dest="beyond_mall", action="store_false",
+                   help="skip the 8M-env (state past the MALL) step-mode supplement that carries the HBM roofline")
+    p.add_argument("--no-probe", dest="probe", action="store_false", help="skip the memory-floor probe")
     p.add_argument("--dist-backend", default="nccl",
                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
                         "ranks share one GPU for rehearsals")
+    p.add_argument("--check-launch", action="store_true",
+                   help="multi-rank plumbing only (process group, barrier, max over ranks, the JSON line): no GPU work")
     return p.parse_args()
 
 
@@ -63,6 +79,17 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     return world, rank, local
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without torch.distributed.run: start it as a CHILD process (nothing here has
+    touched a GPU) with N ranks on this node and return its exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
 
 
 def cpu_baseline(net, seconds: float):
@@ -89,28 +116,80 @@ def cpu_baseline(net, seconds: float):
             "reference_python_1core_measured_in_build_container": "20-28k env-steps/s (BASELINE.md)"}
 
 
-def beyond_mall_supplement(net, device, seed):
-    """Step mode on 8,388,608 envs on ONE GPU (BASELINE config 4's whole batch): 256 MiB of
-    state, past the 256 MB MALL, so every launch streams the state from HBM. Algorithmic bytes
-    / HIP-event kernel time, as for the main line."""
+def read_pmc(path: str, key: str):
+    """Committed PMC results (profiles/): per-launch HBM-side bytes for network:batch, or None."""
+    try:
+        pmc = json.loads(Path(path).read_text())
+    except (OSError, ValueError):
+        return None, None
+    return pmc.get("per_launch_bytes", {}).get(key), pmc.get("source")
+
+
+class MemFloor:
+    """tools/libmallprobe.so: the step kernel's memory pattern without compute (see mall_probe.hip)."""
+
+    def __init__(self):
+        self.lib = ctypes.CDLL(str(ROOT / "tools" / "libmallprobe.so"))
+        self.lib.mall_probe.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double)]
+
+    def us_per_launch(self, n_envs: int, write_pct: int, launches: int) -> float:
+        us = ctypes.c_double()
+        rc = self.lib.mall_probe(n_envs, write_pct, 1, launches, ctypes.byref(us))
+        if rc:
+            raise RuntimeError(f"mall_probe failed: {rc}")
+        return us.value
+
+
+def changed_fraction(batch) -> float:
+    """Fraction of envs whose updated node changed value in one step (the dirty-store kernel
+    writes exactly those envs back): two host copies of the state around one launch."""
+    import numpy as np
+
+    a = batch.get_state()
+    batch.step(1)
+    b = batch.get_state()
+    return float(np.any(a != b, axis=1).mean())
+
+
+def step_run(net, B, device, seed, warmup, steps, env_base=0):
+    """W + K step launches on a fresh batch; K timed with HIP events on the batch stream."""
     from gym_pbn_amd.batch import PBNBatch
 
-    B = 1 << 23
-    b = PBNBatch(net, B, device=device, seed=seed)
+    b = PBNBatch(net, B, device=device, seed=seed, env_id_base=env_base)
     b.randomize()
-    b.step(20)
+    b.step(warmup)
     b.sync()
     b.timing(2)
-    n = 100
-    b.step(n)
+    b.step(steps)
     b.timing(0)
     ms, launches = b.timing_read()
+    return b, ms / 1e3 / max(launches, 1)
+
+
+def beyond_mall_supplement(net, device, seed, floor):
+    """Step mode on 8,388,608 envs on ONE GPU (BASELINE config 4's whole batch): 256 MiB of
+    state, as large as the 256 MiB MALL, so every launch streams the state from HBM. Algorithmic
+    bytes (64 B per update) / HIP-event kernel time against the 8 TB/s HBM spec."""
+    B = 1 << 23
+    b, s = step_run(net, B, device, seed, 50, 200)
+    frac_dirty = changed_fraction(b)
     b.close()
-    s = ms / 1e3 / max(launches, 1)
     alg = 16 * net.n_words * B
-    return {"workload": "Bittner-200 step mode, 8,388,608 envs on one GPU (state 256 MiB > MALL)",
-            "env_steps_per_s": B / s, "avg_kernel_us": s * 1e6, "alg_bytes_per_launch": alg,
-            "achieved_GBs": alg / s / 1e9, "frac": alg / s / 1e9 / HBM_PEAK_GBS}
+    out = {"workload": "Bittner-200 step mode, 8,388,608 envs on one GPU (state 256 MiB, past the MALL)",
+           "bound": "hbm", "achieved": alg / s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": alg / s / 1e9 / HBM_PEAK_GBS, "avg_kernel_us": s * 1e6, "launches_timed": 200,
+           "alg_bytes_per_launch": alg, "env_steps_per_s": B / s, "changed_env_frac": frac_dirty}
+    traffic, src = read_pmc(str(ROOT / "profiles" / "pmc_traffic.json"), f"{net.name}:{B}")
+    out["traffic"] = traffic
+    if traffic:
+        out["traffic_GBs"] = traffic / s / 1e9
+        out["traffic_frac"] = traffic / s / 1e9 / HBM_PEAK_GBS
+    if floor is not None:
+        fl = floor.us_per_launch(B, round(100 * frac_dirty), 50)
+        out["floor_us"] = fl
+        out["frac_of_floor"] = fl / (s * 1e6)
+    return out
 
 
 def copy_bandwidth(device, gib: float = 2.0, reps: int = 10):
@@ -139,19 +218,10 @@ def config2_supplement(device):
     """BASELINE config 2 beside the main line: Bittner-28 (predictor_sets_28_15_median, N = 28,
     one state word), 65,536 envs on one GPU (512 KiB of state: launch-bound in step mode), step
     mode (one Graph.step per env per launch) and rollout (256 updates per launch)."""
-    from gym_pbn_amd.batch import PBNBatch
     from gym_pbn_amd.network import load_network
 
     B = 65536
-    b = PBNBatch(load_network("bittner28"), B, device=device, seed=0x5EED)
-    b.randomize()
-    b.step(500)
-    b.sync()
-    b.timing(2)
-    n = 2000
-    b.step(n)
-    b.timing(0)
-    ms, launches = b.timing_read()
+    b, s = step_run(load_network("bittner28"), B, device, 0x5EED, 500, 2000)
     b.rollout(256)
     b.sync()
     b.timing(2)
@@ -162,12 +232,48 @@ def config2_supplement(device):
     lanes = b.info()["roll_lanes"]
     b.close()
     return {"workload": "Bittner-28, 65,536 envs, 1 GPU (BASELINE config 2)",
-            "step_env_steps_per_s": B * n / (ms / 1e3), "step_us_per_launch": ms * 1e3 / max(launches, 1),
+            "step_env_steps_per_s": B / s, "step_us_per_launch": s * 1e6,
             "rollout_updates_per_launch": 256, "rollout_node_updates_per_s": B * 256 * 5 / (rms / 1e3),
             "rollout_lanes_per_env": lanes}
 
 
-def r6_supplement(args, world, rank, device, dist):
+def rollout_supplement(net, B, device, seed, T, valu):
+    """Rollout mode (T updates per launch, state in the LDS plane): VALU-bound."""
+    from gym_pbn_amd.batch import PBNBatch
+
+    b = PBNBatch(net, B, device=device, seed=seed)
+    b.randomize()
+    b.rollout(T)
+    b.sync()
+    b.timing(2)
+    reps = 5
+    for _ in range(reps):
+        b.rollout(T)
+    b.timing(0)
+    rms, rl = b.timing_read()
+    b.close()
+    s = rms / 1e3 / max(rl, 1)
+    out = {"updates_per_launch": T, "node_updates_per_s_per_gpu": B * T / s, "kernel_ms": s * 1e3}
+    v = (valu or {}).get(f"k_rollout:{net.name}:{B}:{T}")
+    if v:
+        out["roofline"] = valu_roofline(v, s, B * T)
+    return out
+
+
+def valu_roofline(v, s, updates):
+    """VALU roofline: VALU wave-instructions per node update from committed SQ counters
+    (profiles/r02_valu_pmc.json, tools/valu_pmc.py: SQ_INSTS_VALU over a profiled launch of the
+    same kernel, batch and seeds / its node updates) x this run's node updates / its kernel time,
+    against the chip's VALU issue peak (64 lanes per wave-instruction)."""
+    ipu = v["valu_wave_insts_per_update"]
+    lane_ops = ipu * updates * 64
+    return {"bound": "valu", "achieved": lane_ops / s / 1e12, "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
+            "frac": lane_ops / s / 1e12 / VALU_PEAK_TOPS, "valu_wave_insts_per_update": ipu,
+            "valu_busy_frac": v.get("valu_busy_frac"), "kernel_s": s, "node_updates": updates,
+            "source": v.get("source", "profiles/r02_valu_pmc.json")}
+
+
+def r6_supplement(args, world, rank, device, dist, valu):
     """BASELINE config 5 beside the main line: the multi-flip until-attractor env
     (pbn_target_multi.py:119-154) on Bittner-200, ``--r6-batch`` envs per GPU (131,072: 1M
     over 8 GPUs), T = horizon = 100 env steps per chunk written to a device chunk and
@@ -181,7 +287,7 @@ def r6_supplement(args, world, rank, device, dist):
     from gym_pbn_amd.rollout import TrajectoryCollector, gather_chunk
     from gym_pbn_amd.shard import max_over_ranks, shard_for
 
-    T, B, A = 100, args.r6_batch, 4
+    T, B, A, CAP = 100, args.r6_batch, 4, 4096
     z = np.load(ROOT / "tests" / "golden" / "r6_bittner199.npz", allow_pickle=False)
     net = Net(load_network("bittner199"))
     cfg = EnvConfig(net, attractors_from_cubes(z["cube_care"], z["cube_value"], z["cube_attractor"], net.n_nodes),
@@ -195,40 +301,59 @@ def r6_supplement(args, world, rank, device, dist):
 
     def run(fused):
         b = PBNBatch(net, B, device=device, env_id_base=sh.env_base, seed=0xAC7)
-        col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=4096, dist=dist, fused=fused)
+        col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=CAP, dist=dist, fused=fused)
         col.step_chunk(acts)  # warm-up chunk
         col.finish()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         ups = torch.zeros((), dtype=torch.int64, device=dev)
+        stats = []
+        b.timing(1)  # an event pair around every launch on the batch stream: kernel time alone
         t0 = time.perf_counter()
         for _ in range(args.r6_chunks):
             buf, _ = col.step_chunk(acts)
-            ups += buf["n_updates"].to(torch.int64).sum()
+            n = buf["n_updates"]
+            ups += n.to(torch.int64).sum()
+            # per env step: the slowest env (a per-step launch waits for it) and the mean; capped envs
+            stats.append(torch.stack([n.max(dim=1).values.to(torch.float64), n.to(torch.float64).mean(dim=1),
+                                      ((buf["flags"] & 4) != 0).to(torch.float64).mean(dim=1)]))
         col.finish()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         dt = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
+        kms, _ = b.timing_read()
+        b.timing(0)
+        local_ups = float(ups.item())
         if dist is not None:
             dist.all_reduce(ups)
-        lanes = b.info()["env_lanes"]
-        return b, buf, dt, float(ups.item()), lanes
+        st = torch.cat(stats, dim=1).cpu().numpy()
+        tail = {"capped_frac": float(st[2].mean()), "mean_updates_per_env_step": float(st[1].mean()),
+                "max_updates_per_env_step_mean_over_steps": float(st[0].mean()),
+                "steps_whose_slowest_env_hit_the_cap": float((st[0] >= CAP).mean())}
+        return b, buf, dt, float(ups.item()), tail, (kms / 1e3, local_ups)
 
     # closed-loop shape first (one launch per env step, as an agent in the loop needs), then the
     # open-loop collector (actions known for the chunk: one launch walks each env through T steps)
-    b, buf, dt_step, ups_step, _ = run(False)
+    b, buf, dt_step, ups_step, tail_step, k_step = run(False)
     b.close()
-    b, buf, dt, ups, lanes = run(True)
+    b, buf, dt, ups, tail, k_fused = run(True)
+    lanes = b.info()["env_lanes"]
     out = {"metric": "R6 env-steps/s (whole node) incl. per-chunk trajectory all-gather", "unit": "env-steps/s",
            "value": world * B * T * args.r6_chunks / dt, "node_updates_per_s": ups / dt,
            "launch": "one per chunk (T env steps per env in one launch; actions known for the chunk)",
            "value_one_launch_per_env_step": world * B * T * args.r6_chunks / dt_step,
            "node_updates_per_s_one_launch_per_env_step": ups_step / dt_step,
-           "batch_per_gpu": B, "global_batch": world * B, "T": T, "A": A, "update_cap": 4096, "env_lanes": lanes,
-           "chunks": args.r6_chunks, "s_per_chunk": dt / args.r6_chunks,
+           "batch_per_gpu": B, "global_batch": world * B, "T": T, "A": A, "update_cap": CAP, "env_lanes": lanes,
+           "chunks": args.r6_chunks, "s_per_chunk": dt / args.r6_chunks, "tail": tail,
+           "tail_one_launch_per_env_step": tail_step,
            "chunk_bytes_per_gpu": sum(t.numel() * t.element_size() for t in buf.values())}
+    for key, (ks, nu), name in ((f"k_env:bittner199:{B}:fused{T}", k_fused, "roofline"),
+                                (f"k_env:bittner199:{B}:per_step", k_step, "roofline_one_launch_per_env_step")):
+        vr = (valu or {}).get(key)
+        if vr and ks > 0:  # this rank's env kernels: node updates / summed kernel time (HIP events)
+            out[name] = valu_roofline(vr, ks, nu)
     if dist is not None:  # the gather alone: bytes received per GPU / time
         torch.cuda.synchronize()
         dist.barrier()
@@ -242,108 +367,164 @@ def r6_supplement(args, world, rank, device, dist):
     return out
 
 
+def guarded(fn, *a):
+    try:
+        return fn(*a)
+    except Exception as exc:  # a supplement must not cost the main line
+        return {"error": f"{type(exc).__name__}: {exc}"}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, local = dist_env()
-    import numpy as np
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     import torch
 
-    from gym_pbn_amd import _lib
-    from gym_pbn_amd.batch import PBNBatch
-    from gym_pbn_amd.network import load_network
     from gym_pbn_amd.shard import max_over_ranks, shard_for
 
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        ndev = max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local % ndev)
+        if not args.check_launch:
+            ndev = max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local % ndev)
         dist.init_process_group(args.dist_backend)
-    device = (local % max(torch.cuda.device_count(), 1)) if world > 1 else 0
-    if torch.cuda.is_available():
-        torch.cuda.set_device(device)
+    if args.check_launch:  # plumbing only: the N-rank path without GPU work
+        if dist is not None:
+            dist.barrier()
+        t = max_over_ranks(float(rank), dist)
+        if rank == 0:
+            print(json.dumps({"check_launch": True, "n_gpus": dist.get_world_size() if dist else 1,
+                              "max_over_ranks_of_rank": t, "value": None}), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
+    from gym_pbn_amd import _lib  # noqa: F401  (fails loudly when libpbnsim.so is missing)
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.network import load_network
+
+    device = (local % max(torch.cuda.device_count(), 1)) if world > 1 else 0
+    torch.cuda.set_device(device)
     net = load_network(args.network)
     B = args.batch
     shard = shard_for(rank, world, B)  # contiguous global env ids; Philox keyed by global id
-    batch = PBNBatch(net, B, device=device, env_id_base=shard.env_base, seed=args.seed)
-    batch.randomize()
-    batch.sync()
 
     if args.kernel_only:
+        batch = PBNBatch(net, B, device=device, env_id_base=shard.env_base, seed=args.seed)
+        batch.randomize()
         batch.step(args.warmup + args.steps)
         batch.sync()
         return
 
+    try:
+        valu = json.loads(Path(args.valu_file).read_text()).get("kernels", {})
+    except (OSError, ValueError):
+        valu = {}
+    floor = None
+    if args.probe:
+        try:
+            floor = MemFloor()
+        except OSError:
+            floor = None
+
+    # ---- supplements first (every rank, so every GPU enters the headline in the same clock state)
+    sup = {}
+    if args.rollout > 1:
+        sup["rollout"] = guarded(rollout_supplement, net, B, device, args.seed, args.rollout, valu)
+    if args.config2:
+        sup["config2_bittner28"] = guarded(config2_supplement, device)
+    if args.beyond_mall and B == 1 << 20:
+        sup["beyond_mall_8m"] = guarded(beyond_mall_supplement, net, device, args.seed, floor)
+    if args.r6_chunks > 0:
+        sup["config5_r6"] = guarded(r6_supplement, args, world, rank, device, dist, valu)
+    copy = guarded(copy_bandwidth, device) if rank == 0 else None
+
+    # ---- the headline: W warm-up launches, then exactly K timed launches
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    batch = PBNBatch(net, B, device=device, env_id_base=shard.env_base, seed=args.seed)
+    batch.randomize()
     batch.step(args.warmup)
     batch.sync()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    if not args.no_events:
-        batch.timing(2)  # HIP events on the batch stream bracketing the timed launches
+    batch.timing(2)  # HIP events on the batch stream bracketing the timed launches
     t0 = time.perf_counter()
     batch.step(args.steps)
-    if not args.no_events:
-        batch.timing(0)  # closes the event region right behind the last launch
+    batch.timing(0)  # closes the event region right behind the last launch
     batch.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    kernel_ms, launches = batch.timing_read() if not args.no_events else (float("nan"), 0)
+    kernel_ms, launches = batch.timing_read()
     elapsed = max_over_ranks(t1 - t0, dist, device=f"cuda:{device}")
     kernel_ms = max_over_ranks(kernel_ms, dist, device=f"cuda:{device}")
 
-    # supplementary: rollout mode (several updates per launch, state in registers)
-    rollout = None
-    if args.rollout > 1:
-        batch.rollout(args.rollout)
-        batch.sync()
-        batch.timing(2)
-        reps = 5
-        for _ in range(reps):
-            batch.rollout(args.rollout)
-        batch.timing(0)
-        rms, rl = batch.timing_read()
-        rollout = {"updates_per_launch": args.rollout,
-                   "node_updates_per_s_per_gpu": B * args.rollout * reps / (rms / 1e3),
-                   "kernel_ms": rms / max(rl, 1)}
-
-    beyond = None
-    if rank == 0 and args.beyond_mall and B == 1 << 20:
+    # memory floor of the same pattern, same clock state: one pass over the state per launch,
+    # 32 B read per env, the changed envs' 32 B written back
+    dirty = changed_fraction(batch)
+    batch.close()
+    floor_us = None
+    if floor is not None:
         try:
-            beyond = beyond_mall_supplement(net, device, args.seed)
-        except Exception as exc:  # a supplement must not cost the main line
-            beyond = {"error": f"{type(exc).__name__}: {exc}"}
+            floor_us = floor.us_per_launch(B, round(100 * dirty), max(args.steps, 200))
+        except RuntimeError:
+            floor_us = None
 
     W = net.n_words
     alg_bytes = 16 * W * B  # read + write the packed state of every env
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
     achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
-    traffic = None
-    pmc_src = None
-    try:
-        pmc = json.loads(Path(args.pmc_file).read_text())
-        key = f"{args.network}:{B}"
-        if key in pmc.get("per_launch_bytes", {}):
-            traffic = pmc["per_launch_bytes"][key]
-            pmc_src = pmc.get("source")
-    except (OSError, ValueError):
-        pass
-
+    traffic, pmc_src = read_pmc(args.pmc_file, f"{args.network}:{B}")
     total_steps = world * B * args.steps
     value = total_steps / elapsed
     if rank == 0:
+        peak = alg_bytes / (floor_us * 1e-6) / 1e9 if floor_us else None
+        rf = {
+            "bound": "mall",
+            "achieved": achieved,
+            "peak": peak,
+            "unit": "GB/s",
+            "frac": (achieved / peak) if (achieved and peak) else None,
+            "traffic": traffic,
+            "kernel": f"pbn::k_step<{W},1,1,0,1024> (predictor mix, dirty store, Philox, 1024-thread groups)",
+            "alg_bytes_per_launch": alg_bytes,
+            "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
+            "timing": "HIP events on the batch stream bracketing the K timed launches",
+            "residency": "the 32 MiB state stays in the 256 MiB Infinity Cache (MALL) and the XCDs' L2 between "
+                         "launches; the HBM-bound figure is hbm_8m",
+            "peak_source": "memory floor measured live right after the timed launches: tools/mall_probe.hip, the "
+                           "same launch shape (1024-thread groups, 2 per CU, env pairs), 32 B read per env and the "
+                           "changed envs' 32 B written back, no compute; peak = alg_bytes / floor time "
+                           "(MI355X_MICROARCH.md gives no Infinity-Cache streaming figure)",
+            "floor_us": floor_us,
+            "changed_env_frac": dirty,
+            "frac_of_hbm_spec": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic_source": pmc_src,
+            "traffic_GBs": (traffic / avg_kernel_s / 1e9) if (traffic and launches) else None,
+        }
+        bm = sup.get("beyond_mall_8m")
+        if bm and "error" not in bm:
+            rf["hbm_8m"] = {k: bm.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                   "traffic_frac", "avg_kernel_us", "floor_us", "frac_of_floor")}
+        if isinstance(copy, float):
+            rf["achievable_copy_GBs"] = copy
+            rf["achievable_copy_source"] = "torch device-to-device copy of 2 GiB (past the MALL), read + write bytes"
         out = {
             "metric": "env-steps/sec (whole node), Bittner-200, batch=1M; achieved HBM GB/s",
             "value": value,
             "unit": "env-steps/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if dist is not None else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
@@ -355,65 +536,22 @@ def main():
                     "predictor_sets_200_5_kmeans.pkl)",
             "config": {
                 "workload": "Bittner-200 async node update (R1 Graph.step), step mode: one update per env per "
-                            "launch, state resident in HBM",
+                            "launch, state resident in device memory",
                 "network": args.network, "n_nodes": net.n_nodes, "state_words": W,
                 "batch_per_gpu": B, "global_batch": world * B, "updates_per_step": 1,
                 "parallelism": f"dp{world} (env shards, no collective)", "rng": "philox4x32-10",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": traffic,
-                "kernel": "pbn::k_step<4,1,1,0,1024> (W=4, predictor mix, dirty store, Philox, 1024-thread groups)",
-                "timing": "HIP events on the batch stream bracketing the timed launches (launch gaps included)",
-                "alg_bytes_per_launch": alg_bytes,
-                "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
-                "traffic_source": pmc_src,
-                # measured HBM-side bytes per launch / launch time: the kernel stores only the
-                # envs that changed and re-reads a 32 MiB state the 256 MB MALL can hold,
-                # so the algorithmic rate above can exceed the HBM peak
-                "traffic_GBs": (traffic / avg_kernel_s / 1e9) if (traffic and launches) else None,
-                "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if (traffic and launches) else None,
-            },
+            "roofline": rf,
             "node_updates_per_s": value,
-            "rollout": rollout,
-            "beyond_mall_8m": beyond,
+            "order": "supplements (rollout, config 2, 8M past-MALL, config 5) ran before the headline",
+            **sup,
         }
-    batch.close()
-    cfg2 = None
-    if rank == 0 and args.config2:
-        try:
-            cfg2 = config2_supplement(device)
-        except Exception as exc:  # a supplement must not cost the main line
-            cfg2 = {"error": f"{type(exc).__name__}: {exc}"}
-    r6 = None
-    if args.r6_chunks > 0:
-        try:
-            r6 = r6_supplement(args, world, rank, device, dist)
-        except Exception as exc:  # a supplement must not cost the main line
-            r6 = {"error": f"{type(exc).__name__}: {exc}"}
-    if rank == 0:
-        try:  # achievable-copy rate on this box beside the spec peak
-            copy = copy_bandwidth(device)
-            rf = out["roofline"]
-            rf["achievable_copy_GBs"] = copy
-            rf["achievable_copy_source"] = ("torch device-to-device copy of 2 GiB (past the MALL), read + write "
-                                            "bytes / CUDA-event time; the kernel's traffic_GBs also counts "
-                                            "MALL-served fetches, so it can exceed this")
-        except Exception as exc:  # a supplement must not cost the main line
-            out["roofline"]["achievable_copy_GBs"] = f"error: {type(exc).__name__}: {exc}"
-        out["config2_bittner28"] = cfg2
-        out["config5_r6"] = r6
-        if not args.no_cpu_baseline and world == 1:  # the host-core baseline: rank 0 at N = 1 only
+        if world == 1 and not args.no_cpu_baseline:  # the host-core baseline: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(net, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    del np, _lib
 
 
 if __name__ == "__main__":

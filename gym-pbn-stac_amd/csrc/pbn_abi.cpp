@@ -138,6 +138,9 @@ struct pbn_envcfg {
     }
 };
 
+constexpr uint32_t STEP_GRAPH_K = 64;  // longest captured run of step launches
+constexpr int STEP_GRAPH_SIZES = 6;     // graphs of 64, 32, 16, 8, 4 and 2 launches
+
 struct pbn_batch {
     pbn_net* net = nullptr;
     int device = 0, W = 0, N = 0;
@@ -146,6 +149,7 @@ struct pbn_batch {
     uint64_t B = 0, env_base = 0, seed = 0, update_count = 0;
     uint32_t env_calls = 0, reset_count = 0;
     int env_lanes = 0;  // lanes per env of the last R6 launch
+    int env_grid_last = 0;  // workgroups of the last R6 launch
     uint64_t* d_state = nullptr;
     int64_t* d_nsteps = nullptr;
     int32_t* d_error = nullptr;
@@ -158,13 +162,17 @@ struct pbn_batch {
     bool env_no_gen = false;  // PBNSIM_ENV_NO_GEN: no cooperative draw generation
     int env_group = 0;        // PBNSIM_ENV_GROUP: lanes per env (1 = lane mode), 0 = by batch size
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
+    int env_grid_cap = 0;     // PBNSIM_ENV_GRID: cap on the R6 kernel's workgroups (tests: lane refill), 0 = none
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
                               // count, -1 = by size
     int roll_group = 1;       // PBNSIM_ROLL_GROUP: lanes per env of the rollout kernel (default by size)
     bool step_graph_off = false;  // PBNSIM_STEP_GRAPH=0: step mode without HIP graphs
-    hipGraphExec_t step_graph = nullptr;  // STEP_GRAPH_K step launches + k_bump, captured once
+    // step_graph[j]: (STEP_GRAPH_K >> j) step launches + k_bump, captured once (all sizes at the
+    // first call of two or more steps)
+    hipGraphExec_t step_graph[STEP_GRAPH_SIZES] = {};
+    bool step_graph_built = false;
     bool step_graph_broken = false;       // capture or instantiation failed once: plain launches
     DevBuf s_ubase;                       // device copy of update_count for graph replays
     DevBuf s_flip_err;                    // range-error flag of pbn_flip_device
@@ -437,6 +445,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
     if (const char* v = getenv("PBNSIM_ENV_GROUP")) b->env_group = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
+    if (const char* v = getenv("PBNSIM_ENV_GRID")) b->env_grid_cap = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -488,7 +497,8 @@ void pbn_batch_destroy(pbn_batch* b) {
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
                       &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase, &b->s_flip_err})
         d->release();
-    if (b->step_graph) (void)hipGraphExecDestroy(b->step_graph);
+    for (hipGraphExec_t& g : b->step_graph)
+        if (g) (void)hipGraphExecDestroy(g);
     b->pin.release();
     if (b->own_stream) {
         (void)hipStreamSynchronize(b->stream);
@@ -523,6 +533,7 @@ int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
     info->mt_ready = b->mt_ready;
     info->env_lanes = b->env_lanes;
     info->roll_lanes = b->roll_group;
+    info->env_grid = b->env_grid_last;
     return 0;
 }
 
@@ -729,32 +740,41 @@ static int step_launch(pbn_batch* b, uint32_t T, uint64_t update_base, int repla
     return timed ? b->ev_end(stop) : 0;
 }
 
-// Step mode is launch-bound between kernels (one HBM pass each): runs of STEP_GRAPH_K launches
-// go out as one captured HIP graph -- the same kernels with the same arguments, except that the
-// update counter comes from device memory (*ubase + k for launch k; k_bump adds STEP_GRAPH_K
-// at the end of the graph), so one instantiated graph serves every replay.
-constexpr uint32_t STEP_GRAPH_K = 64;
-
+// Step mode is launch-bound between kernels (one HBM pass each): runs of step launches go out
+// as captured HIP graphs -- the same kernels with the same arguments, except that the update
+// counter comes from device memory (*ubase + k for launch k; k_bump adds the graph's length at
+// its end), so one instantiated graph per length serves every replay. Lengths 64, 32, ..., 2 are
+// all captured at the first call of two or more steps; a call of n steps replays 64-graphs, then
+// the binary digits of the rest (n = 20: the 16- and the 4-graph), then one plain launch if n is odd.
 static bool step_graph_ready(pbn_batch* b) {
-    if (b->step_graph) return true;
+    if (b->step_graph_built) return true;
     if (b->step_graph_broken || b->step_graph_off || !b->stream) return false;  // the null stream cannot capture
     if (b->s_ubase.ensure(64)) return false;
-    hipGraph_t g = nullptr;
-    bool ok = hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
-    bool launched = ok;
-    for (uint32_t k = 0; launched && k < STEP_GRAPH_K; ++k)
-        launched = step_launch(b, 1, k, 0, nullptr, nullptr, (const uint64_t*)b->s_ubase.p, false) == 0;
-    if (launched) launched = launch_bump((uint64_t*)b->s_ubase.p, STEP_GRAPH_K, b->stream) == 0;
-    if (ok) ok = hipStreamEndCapture(b->stream, &g) == hipSuccess && launched && g;
-    if (ok) ok = hipGraphInstantiate(&b->step_graph, g, nullptr, nullptr, 0) == hipSuccess;
-    if (g) (void)hipGraphDestroy(g);
+    bool ok = true;
+    for (int j = 0; ok && j < STEP_GRAPH_SIZES; ++j) {
+        const uint32_t K = STEP_GRAPH_K >> j;
+        hipGraph_t g = nullptr;
+        ok = hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        bool launched = ok;
+        for (uint32_t k = 0; launched && k < K; ++k)
+            launched = step_launch(b, 1, k, 0, nullptr, nullptr, (const uint64_t*)b->s_ubase.p, false) == 0;
+        if (launched) launched = launch_bump((uint64_t*)b->s_ubase.p, K, b->stream) == 0;
+        if (ok) ok = hipStreamEndCapture(b->stream, &g) == hipSuccess && launched && g;
+        if (ok) ok = hipGraphInstantiate(&b->step_graph[j], g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+    }
     if (!ok) {
-        b->step_graph = nullptr;
+        for (hipGraphExec_t& g : b->step_graph) {
+            if (g) (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
         b->step_graph_broken = true;
         (void)hipGetLastError();  // the failed capture is not the caller's error
         g_err.clear();
+        return false;
     }
-    return ok;
+    b->step_graph_built = true;
+    return true;
 }
 
 int pbn_step(pbn_batch* b, uint32_t n_updates) {
@@ -764,18 +784,23 @@ int pbn_step(pbn_batch* b, uint32_t n_updates) {
     // not while the caller is capturing the stream into a graph of its own: plain launches then
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (b->stream && hipStreamIsCapturing(b->stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
-    if (n_updates >= STEP_GRAPH_K && b->timing != 1 && cap == hipStreamCaptureStatusNone && step_graph_ready(b)) {
+    const uint32_t smallest = STEP_GRAPH_K >> (STEP_GRAPH_SIZES - 1);
+    if (n_updates >= smallest && b->timing != 1 && cap == hipStreamCaptureStatusNone && step_graph_ready(b)) {
         // device counter <- update_count (two 32-bit memsets: stream-ordered, no host buffer)
         uint32_t* c = (uint32_t*)b->s_ubase.p;
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c, (int)(uint32_t)b->update_count, 1, b->stream));
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c + 1), (int)(uint32_t)(b->update_count >> 32), 1, b->stream));
-        for (; t + STEP_GRAPH_K <= n_updates; t += STEP_GRAPH_K) {
-            hipEvent_t stop;
-            if (int rc = b->ev_begin(&stop)) return rc;
-            if (b->timing == 2) b->region_launches += STEP_GRAPH_K - 1;  // ev_begin counted one
-            HIP_TRY(hipGraphLaunch(b->step_graph, b->stream));
-            if (int rc = b->ev_end(stop)) return rc;
-            b->update_count += STEP_GRAPH_K;
+        for (int j = 0; j < STEP_GRAPH_SIZES; ++j) {
+            const uint32_t K = STEP_GRAPH_K >> j;
+            while (n_updates - t >= K && (j == 0 || n_updates - t < 2 * K)) {
+                hipEvent_t stop;
+                if (int rc = b->ev_begin(&stop)) return rc;
+                if (b->timing == 2) b->region_launches += K - 1;  // ev_begin counted one
+                HIP_TRY(hipGraphLaunch(b->step_graph[j], b->stream));
+                if (int rc = b->ev_end(stop)) return rc;
+                b->update_count += K;
+                t += K;
+            }
         }
     }
     for (; t < n_updates; t++) {
@@ -1194,11 +1219,14 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     HIP_TRY(hipMemsetAsync(b->s_counter.p, 0, 8, b->stream));
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
-    int e = launch_env_multi(b->W, a, replay, b->grid_for(b->B * (uint64_t)grp, bpc), b->stream);
+    int grid = b->grid_for(b->B * (uint64_t)grp, bpc);
+    if (b->env_grid_cap) grid = std::min(grid, b->env_grid_cap);  // persistent waves: any grid drains the counter
+    int e = launch_env_multi(b->W, a, replay, grid, b->stream);
     if (e) return fail(PBN_E_HIP, "k_env launch: %s", hipGetErrorString((hipError_t)e));
     if (int rc = b->ev_end(stop)) return rc;
     if (!replay) b->env_calls += n_calls;
     b->env_lanes = grp;
+    b->env_grid_last = grid;
     return 0;
 }
 

@@ -59,8 +59,43 @@ def _general(N=200, all_attractors=None, **kw):  # pbn_target_multi.py:531-536 (
     return envs.PBNTargetMultiEnv(net, all_attractors, **kw)
 
 
+def _pbn_target(graph=None, goal_config=None, render_mode=None, render_no_cache=False, name=None,
+                reward_config=None, end_episode_on_success=False, *, all_attractors=None, **kw):
+    """``gym-PBN/PBN-target-v0`` -> ``PBNTargetEnv`` (``gym_PBN/__init__.py:5``) with the reference
+    constructor (``pbn_target.py:26-110``): ``graph`` (here a network: a ``PredictorNetwork`` or a
+    bundled name), ``goal_config`` with ``target_nodes`` / ``target_node_values`` /
+    ``undesired_node_values`` / ``intervene_on`` (more than one missing raises, as ``_check_config``
+    does; an empty config raises ``ValueError``), optional ``goal_config["horizon"]`` (default 100),
+    ``reward_config`` (defaults 10 / 2 / 1; kept as attributes -- the reward itself is +20 / -5,
+    ``:303-326``). The base class starts with no attractors (``:101``), so ``reset`` could never run
+    there; here they are the keyword ``all_attractors`` (cabean output), required."""
+    if graph is None:
+        raise TypeError("PBNTargetEnv() missing required argument: 'graph'")
+    goal_config = envs.PBNEnv._check_config(
+        goal_config, "goal", {"target_nodes", "target_node_values", "undesired_node_values", "intervene_on"})
+    if goal_config is None:
+        raise ValueError("Target nodes, target values and intervention nodes need to be specified.")
+    reward_config = envs.PBNEnv._check_config(
+        reward_config, "reward", {"successful_reward", "wrong_attractor_cost", "action_cost"},
+        default_values={"successful_reward": 10, "wrong_attractor_cost": 2, "action_cost": 1})
+    if all_attractors is None:
+        raise ValueError("all_attractors is required (cabean output; see gym_pbn_amd.io.cabean)")
+    env = envs.PBNTargetEnv(graph, all_attractors, horizon=goal_config.get("horizon", 100), name=name, **kw)
+    env.target_nodes = goal_config.get("target_nodes")
+    env.target_node_values = goal_config.get("target_node_values")
+    env.undesired_node_values = goal_config.get("undesired_node_values")
+    env.intervene_on = goal_config.get("intervene_on")
+    env.successful_reward = reward_config["successful_reward"]
+    env.wrong_attractor_cost = reward_config["wrong_attractor_cost"]
+    env.action_cost = reward_config["action_cost"]
+    env.end_episode_on_success = end_episode_on_success
+    env.render_mode, env.render_no_cache = render_mode, render_no_cache
+    return env
+
+
 REGISTRY: Dict[str, Callable] = {
     "gym-PBN/PBN-v0": envs.PBNEnv,
+    "gym-PBN/PBN-target-v0": _pbn_target,
     "gym-PBN/PBN-sampled-data-v0": mdp.PBNSampledDataEnv,
     "gym-PBN/PBN-self-triggering-v0": mdp.PBNSelfTriggeringEnv,
     "gym-PBN/PBCN-v0": mdp.PBCNEnv,

@@ -110,9 +110,7 @@ class TrajectoryCollector:
         """
         i = self._k % 2
         if self._pending[i] is not None:  # the buffer's previous gather must be done before reuse
-            for w in self._pending[i]:
-                w.wait()
-            self._pending[i] = None
+            self._drain(i)
         buf = self.bufs[i]
         if reset:
             self.batch.env_reset(self.cfg)
@@ -124,9 +122,27 @@ class TrajectoryCollector:
         self._k += 1
         return buf, (self.gathered[i] if self.dist is not None else None)
 
+    def _drain(self, i: int) -> None:
+        """Block the host until buffer ``i``'s gather has finished reading it.
+
+        With RCCL (tensors on a GPU) ``Work.wait()`` only makes torch's *current* stream wait for
+        the collective's stream; the host returns at once, and the env kernel that overwrites the
+        buffer next runs on the batch's own stream, which that wait does not order. A rank can be
+        two chunks ahead of a slower peer, so the collective may still be sending the buffer:
+        synchronising the current stream (it now carries the wait) closes that window. The
+        gather was started a whole chunk earlier, so this costs nothing in the steady state.
+        With gloo ``wait()`` already blocks the host.
+        """
+        for w in self._pending[i]:
+            w.wait()
+        self._pending[i] = None
+        buf = self.bufs[i]["obs"]
+        if buf.is_cuda:
+            import torch
+
+            torch.cuda.current_stream(buf.device).synchronize()
+
     def finish(self) -> None:
         for i in range(2):
             if self._pending[i] is not None:
-                for w in self._pending[i]:
-                    w.wait()
-                self._pending[i] = None
+                self._drain(i)

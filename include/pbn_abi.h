@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 8
+#define PBN_ABI_VERSION 9
 
 enum {
     PBN_OK = 0,
@@ -83,6 +83,7 @@ typedef struct {
     int32_t mt_ready; /* 1 after pbn_mt_seed */
     int32_t env_lanes; /* last R6 env-step launch: 1 = one lane per env (k_env), 2/4/8 = lanes per env (k_env_grp) */
     int32_t roll_lanes; /* rollout kernel: 1 = one lane per env (k_rollout), 2/4/8 = lanes per env (k_rollout_grp) */
+    int32_t env_grid;   /* last R6 env-step launch: workgroups (256 lanes each; lanes refill from a work counter) */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).

@@ -76,9 +76,9 @@ def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
 @pytest.mark.parametrize("graph", ["1", "0"])
 @pytest.mark.parametrize("name", ["bittner199", "tt200"])
 def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name):
-    """pbn_step sends runs of 64 launches as one captured HIP graph (update counter read from
-    device memory): replays continue the counter exactly, across calls and mixed with plain
-    launches and rollouts; region timing still counts every launch."""
+    """pbn_step sends runs of launches as captured HIP graphs of 64, 32, ..., 2 launches (update
+    counter read from device memory): replays continue the counter exactly for every run length,
+    across calls and mixed with plain launches and rollouts; region timing counts every launch."""
     monkeypatch.setenv("PBNSIM_STEP_GRAPH", graph)
     net = load_network(name)
     o = oracle_mod.Oracle(net)
@@ -86,7 +86,7 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
     b = G.PBNBatch(net, B, seed=71, env_id_base=13)
     b.randomize()
     init = b.get_state()
-    b.step(64 * 3 + 7)  # three replays + seven plain launches
+    b.step(64 * 3 + 7)  # three 64-replays, then the 4- and 2-graphs and one plain launch
     b.rollout(5)
     b.step(64)
     assert np.array_equal(b.get_state(), o.step_philox(init, 71, 13, 0, 64 * 4 + 12))
@@ -96,6 +96,14 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
     ms, launches = b.timing_read()
     assert launches == 128 and ms > 0
     assert np.array_equal(b.get_state(), o.step_philox(init, 71, 13, 0, 64 * 6 + 12))
+    done = 64 * 6 + 12
+    for n in (1, 2, 3, 5, 20, 63, 127, 1):  # every binary digit of a run below 64 is its own graph
+        b.timing(2)
+        b.step(n)
+        b.timing(0)
+        assert b.timing_read()[1] == n
+        done += n
+        assert np.array_equal(b.get_state(), o.step_philox(init, 71, 13, 0, done)), n
     b.close()
 
 
@@ -243,8 +251,8 @@ def test_full_size_shard_invariance_and_sampled_oracle(G, oracle_mod):
     assert np.array_equal(np.concatenate(halves), got)
     idx = np.random.default_rng(0).choice(B, 2000, replace=False)
     o = oracle_mod.Oracle(net)
-    for e in idx[:50]:
-        assert np.array_equal(o.step_philox(init[e:e + 1], 2024, int(e), 0, T)[0], got[e])
+    for e in idx:
+        assert np.array_equal(o.step_philox(init[e:e + 1], 2024, int(e), 0, T)[0], got[e]), e
     # bits beyond node 198 stay clear
     assert not (got[:, 3] >> np.uint64(199 - 192)).any()
 

@@ -1,0 +1,213 @@
+"""R6 (``PBNTargetMultiEnv.step``, pbn_target_multi.py:119-154) in the regimes the bench numbers
+come from, checked against the oracle (``oracle.env_step_multi``, the CPU restatement).
+
+* Lane refill: ``k_env`` is persistent -- a lane that finishes its env takes the next one from
+  a global work counter. At the bench sizes (131,072 and 1,048,576 envs) every lane handles
+  several envs, mixing envs at different update counts inside one wave's shared draw tables.
+  ``PBNSIM_ENV_GRID`` caps the grid so a few thousand envs put every lane through >= 3 envs:
+  waves start full (>= 40 active lanes: each lane draws its own entries) and end in the tail
+  (< 40: the rank / counter tables of the shared path). All envs are compared.
+* Config 5 per GPU: 131,072 Bittner-199 envs, one T = 100 chunk in one fused launch, equal in
+  full to 100 per-step launches and to the oracle on 2,000 sampled envs.
+
+Production settings: the r6_bittner199 fixture's attractor cubes, A = 4 (0 w.p. 0.75),
+update cap 4,096 (about a fifth of the env steps run into it).
+"""
+
+import numpy as np
+import pytest
+
+from conftest import cubes_to_attractors, golden, r6_config
+from gym_pbn_amd.network import load_network
+
+pytestmark = pytest.mark.gpu
+
+CAP = 4096
+
+
+def _actions(rng, shape, N):
+    a = rng.integers(1, N + 1, size=shape).astype(np.int32)
+    a[rng.random(shape) < 0.75] = 0
+    return a
+
+
+def _setup(G, B, seed, env_base):
+    z = golden("r6_bittner199.npz")
+    net = load_network("bittner199")
+    gnet = G.Net(net)
+    cfg = G.EnvConfig(gnet, cubes_to_attractors(z, net.n_nodes), horizon=100)
+    cfgd = r6_config(z)
+    cfgd["horizon"] = 100
+    b = G.PBNBatch(gnet, B, seed=seed, env_id_base=env_base)
+    b.env_reset(cfg)
+    return net, cfg, cfgd, b
+
+
+@pytest.fixture(scope="module")
+def G():
+    from gym_pbn_amd import _lib, batch
+
+    assert _lib.device_count() >= 1, "gpu tests need a HIP device"
+    return batch
+
+
+@pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step"])
+def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
+    import torch
+
+    grp = "8" if mode.startswith("grp8") else "1"
+    monkeypatch.setenv("PBNSIM_ENV_GROUP", grp)
+    grid = 4 if grp == "1" else 2
+    monkeypatch.setenv("PBNSIM_ENV_GRID", str(grid))
+    B = 6144 if grp == "1" else 1024
+    lanes = grid * 256 // int(grp)  # env slots in flight
+    assert B >= 3 * lanes  # every lane (group) takes >= 3 envs from the work counter
+    seed, base, T, A = 0xAC7, 5000, 3, 4
+    net, cfg, cfgd, b = _setup(G, B, seed, base)
+    o = oracle_mod.Oracle(net)
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfgd["reset_care"],
+                                cfgd["reset_value"], seed=seed, env_base=base, reset_count=0)
+    assert np.array_equal(b.get_state(), st)
+    acts = _actions(np.random.default_rng(17), (T, B, A), net.n_nodes)
+    if mode == "fused":
+        dev = torch.device("cuda", 0)
+        d_a = torch.from_numpy(acts).to(dev)
+        o_ = torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev)
+        r_ = torch.empty((T, B), dtype=torch.int32, device=dev)
+        f_ = torch.empty((T, B), dtype=torch.uint8, device=dev)
+        n_ = torch.empty((T, B), dtype=torch.int32, device=dev)
+        b.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, o_.data_ptr(), r_.data_ptr(), f_.data_ptr(),
+                                   n_.data_ptr(), update_cap=CAP)
+        b.sync()
+        got = [(o_[t].cpu().numpy().view(np.uint64), r_[t].cpu().numpy(), f_[t].cpu().numpy(),
+                n_[t].cpu().numpy().view(np.uint32)) for t in range(T)]
+    else:
+        got = [b.env_step_multi(cfg, acts[t], update_cap=CAP) for t in range(T)]
+    info = b.info()
+    assert info["env_grid"] == grid and info["env_lanes"] == int(grp)
+    capped = 0
+    for t in range(T):
+        ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=CAP)
+        obs, rew, flags, nup = got[t]
+        assert np.array_equal(nup, ref["n_updates"]), t
+        assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), t
+        assert np.array_equal(flags, ref["flags"]), t
+        st, ns = ref["state"], ref["n_steps"]
+        capped += int(((flags & 4) != 0).sum())
+    assert np.array_equal(b.get_state(), st) and np.array_equal(b.get_n_steps(), ns)
+    assert 0 < capped < T * B  # both regimes: envs that hit the cap and envs that reached an attractor
+
+
+def test_config5_chunk_131k_fused_vs_per_step_and_oracle(G, oracle_mod):
+    """BASELINE config 5's per-GPU shard: 131,072 envs, T = 100 env steps. The fused chunk (one
+    launch) equals 100 per-step launches on every env and field; 2,000 envs (20 blocks of 100 at
+    random offsets) equal the oracle step by step."""
+    import torch
+
+    B, T, A, seed, base = 131072, 100, 4, 0xAC7, 3 * 131072  # rank 3 of 8
+    dev = torch.device("cuda", 0)
+    net, cfg, cfgd, b1 = _setup(G, B, seed, base)
+    init = b1.get_state()
+    ns0 = b1.get_n_steps()
+    acts = _actions(np.random.default_rng(99), (T, B, A), net.n_nodes)
+    d_a = torch.from_numpy(acts).to(dev)
+
+    def outs():
+        return (torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev),
+                torch.empty((T, B), dtype=torch.int32, device=dev),
+                torch.empty((T, B), dtype=torch.uint8, device=dev),
+                torch.empty((T, B), dtype=torch.int32, device=dev))
+
+    fo = outs()
+    b1.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, *[x.data_ptr() for x in fo], update_cap=CAP)
+    b1.sync()
+    b2 = G.PBNBatch(cfg.net, B, seed=seed, env_id_base=base)
+    b2.env_reset(cfg)
+    po = outs()
+    for t in range(T):
+        b2.env_step_multi_device(cfg, d_a[t].data_ptr(), A, *[x[t].data_ptr() for x in po], update_cap=CAP)
+    b2.sync()
+    for x, y in zip(fo, po):
+        assert torch.equal(x, y)
+    assert np.array_equal(b1.get_state(), b2.get_state()) and np.array_equal(b1.get_n_steps(), b2.get_n_steps())
+    flags = fo[2].cpu().numpy()
+    nup = fo[3].cpu().numpy()
+    assert (flags[-1] & 2).all()  # truncated at the horizon
+    assert 0.05 < ((flags & 4) != 0).mean() < 0.5 and nup.max() == CAP  # the capped regime is exercised
+    # oracle on 2,000 sampled envs
+    o = oracle_mod.Oracle(net)
+    obs, rew, fl = fo[0].cpu().numpy().view(np.uint64), fo[1].cpu().numpy(), flags
+    starts = np.sort(np.random.default_rng(5).choice(B // 100, 20, replace=False)) * 100
+    for s0 in starts:
+        sl = slice(int(s0), int(s0) + 100)
+        st, ns = init[sl], ns0[sl]
+        for t in range(T):
+            ref = o.env_step_multi(cfgd, st, ns, acts[t, sl], seed=seed, env_base=base + int(s0), call_idx=t,
+                                   update_cap=CAP)
+            assert np.array_equal(nup[t, sl].view(np.uint32), ref["n_updates"]), (s0, t)
+            assert np.array_equal(obs[t, sl], ref["obs"]) and np.array_equal(rew[t, sl], ref["reward"]), (s0, t)
+            assert np.array_equal(fl[t, sl], ref["flags"]), (s0, t)
+            st, ns = ref["state"], ref["n_steps"]
+        assert np.array_equal(b1.get_state()[sl], st)
+
+
+def test_collector_does_not_reuse_a_buffer_still_being_gathered(G):
+    """rollout.TrajectoryCollector double-buffers chunks; with RCCL, ``Work.wait()`` only orders
+    torch's current stream, not the batch stream the env kernel runs on. A stand-in process group
+    whose all-gather reads the chunk late (on a side stream, behind a ~50 ms device sleep) and whose
+    ``wait()`` has RCCL's semantics shows that the gathered copy of chunk 0 is still chunk 0 after
+    chunk 2 has been written into the same buffer."""
+    import torch
+
+    from gym_pbn_amd.rollout import TrajectoryCollector
+
+    dev = torch.device("cuda", 0)
+
+    class _Work:
+        def __init__(self, ev):
+            self.ev = ev
+
+        def wait(self):  # like RCCL: the current stream waits, the host does not
+            torch.cuda.current_stream(dev).wait_event(self.ev)
+
+    class _LateGather:
+        def __init__(self):
+            self.side = torch.cuda.Stream(dev)
+            self.snaps = []
+
+        def is_initialized(self):
+            return True
+
+        def get_world_size(self):
+            return 2
+
+        def all_gather_into_tensor(self, dst, src, async_op=False):
+            self.side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(self.side):
+                torch.cuda._sleep(100_000_000)
+                snap = src.clone()
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self.snaps.append(snap)
+            return _Work(ev)
+
+    z = golden("r6_bittner28.npz")
+    net = G.Net(load_network("bittner28"))
+    cfg = G.EnvConfig(net, cubes_to_attractors(z, 28), horizon=5)
+    B, T, A = 2048, 5, 2
+    acts = torch.from_numpy(_actions(np.random.default_rng(3), (T, B, A), 28)).to(dev)
+    fake = _LateGather()
+    col = TrajectoryCollector(G.PBNBatch(net, B, seed=11), cfg, T, A, dev, update_cap=4096, dist=fake)
+    ref = TrajectoryCollector(G.PBNBatch(net, B, seed=11), cfg, T, A, dev, update_cap=4096)
+    expect = []
+    for _ in range(3):
+        col.step_chunk(acts)
+        buf, _ = ref.step_chunk(acts)
+        torch.cuda.synchronize()
+        expect.append(buf["obs"].clone())
+    col.finish()
+    torch.cuda.synchronize()
+    obs_snaps = fake.snaps[0::4]  # one gather per field, obs first
+    assert not torch.equal(expect[0], expect[2])
+    for k in range(3):
+        assert torch.equal(obs_snaps[k].view(expect[k].shape), expect[k]), k

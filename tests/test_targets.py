@@ -28,6 +28,47 @@ def test_registry_ids_and_required_inputs():
         make("gym-PBN/BittnerMulti-7-v0", all_attractors=[[("*",) * 7]])  # network needs xls inference
 
 
+def test_pbn_target_v0_reference_constructor_checks():
+    """gym-PBN/PBN-target-v0 (gym_PBN/__init__.py:5): the reference constructor's argument checks
+    (pbn_target.py:26-110) run before anything touches the device."""
+    from gym_pbn_amd.registry import REGISTRY, make
+
+    assert "gym-PBN/PBN-target-v0" in REGISTRY
+    goal = {"target_nodes": [0], "target_node_values": ((1,),), "undesired_node_values": ((0,),),
+            "intervene_on": [0, 1]}
+    with pytest.raises(TypeError):
+        make("gym-PBN/PBN-target-v0", goal_config=goal, all_attractors=_atts())  # graph is required
+    with pytest.raises(ValueError, match="need to be specified"):
+        make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config=None, all_attractors=_atts())
+    with pytest.raises(ValueError, match="required values are missing"):
+        make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config={"target_nodes": [0]},
+             all_attractors=_atts())
+    with pytest.raises(ValueError, match="all_attractors"):
+        make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config=goal)
+
+
+@pytest.mark.gpu
+def test_pbn_target_v0_env():
+    """PBN-target-v0 builds the same env as Bittner-28-v0 from the reference kwargs; horizon from
+    goal_config (default 100), reward_config kept, reset reproduces the reference KAT."""
+    from gym_pbn_amd.registry import make
+
+    goal = {"target_nodes": [0], "target_node_values": ((1,),), "undesired_node_values": ((0,),),
+            "intervene_on": [0, 1], "horizon": 3}
+    env = make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config=goal,
+               reward_config={"successful_reward": 7, "wrong_attractor_cost": 3, "action_cost": 2},
+               name="t", all_attractors=_atts(), seed=4)
+    assert env.horizon == 3 and env.successful_reward == 7 and env.intervene_on == [0, 1] and env.name == "t"
+    case = KAT["cases"][0]
+    (st, tg), info = env.reset(seed=case["seed"])
+    assert list(st) == case["state"] and list(tg) == case["target"]
+    for t in range(3):
+        obs, r, term, trunc, info = env.step(1)
+        assert r in (20, -5) and trunc == (t == 2)
+    del goal["horizon"]
+    assert make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config=goal, all_attractors=_atts()).horizon == 100
+
+
 @pytest.mark.gpu
 def test_target_env_reset_matches_reference_and_step_semantics():
     from gym_pbn_amd.registry import make

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r02_valu_pmc.json (copied to
+profiles/ after review; bench.py reads it for the rollout and config-5 rooflines).
+
+One rocprofv3 --pmc pass (kernel trace only; 4 SQ counters + 1 GRBM counter, within one pass's
+limits) over tools/valu_pmc_child.py, which runs the bench line's rollout (1M envs, T = 64) and
+config-5 R6 chunks (131,072 envs, T = 100; fused and one launch per env step) with the bench's
+seeds and logs every launch's node updates. Per kernel configuration:
+  valu_wave_insts_per_update = sum SQ_INSTS_VALU / sum node updates (wave64 instructions)
+  valu_busy_frac             = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (both quad-cycles; the share of
+                               wave time spent issuing VALU)
+  effective_clock_GHz        = GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time (MI355X_MICROARCH.md
+                               'DVFS give-back'; reads high on dispatches under ~0.3 ms)
+The first launch of each configuration is dropped (warm-up). Runs rocprofv3 as a CHILD process.
+"""
+import collections
+import csv
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+COUNTERS = ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+
+
+def main():
+    outdir = ROOT / "gpurun_out" / "valu_pmc"
+    cmd = ["rocprofv3", "--pmc", *COUNTERS, "--kernel-trace", "--output-format", "csv", "-d", str(outdir), "-o",
+           "run", "--", sys.executable, str(ROOT / "tools" / "valu_pmc_child.py")]
+    subprocess.run(cmd, check=True, cwd=str(ROOT))
+    log = json.loads((ROOT / "gpurun_out" / "valu_child.json").read_text())
+    files = list(outdir.rglob("*counter_collection.csv"))
+    rows = list(csv.DictReader(open(files[0])))
+    disp = collections.OrderedDict()
+    for r in rows:
+        name = r["Kernel_Name"]
+        if not ("k_env" in name or "k_rollout" in name):
+            continue
+        d = disp.setdefault(int(r["Dispatch_Id"]), {"name": name, "t": 0.0})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        if "Start_Timestamp" in r and r.get("End_Timestamp"):
+            d["t"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    seq = [disp[k] for k in sorted(disp)]
+    if len(seq) != len(log):
+        raise SystemExit(f"{len(seq)} profiled dispatches vs {len(log)} logged launches")
+    groups = collections.OrderedDict()
+    for d, (kind, key, ups) in zip(seq, log):
+        assert kind in d["name"], (kind, d["name"])
+        groups.setdefault(key, []).append((d, ups))
+    res = {}
+    for key, items in groups.items():
+        items = items[1:] if len(items) > 1 else items  # drop the warm-up launch
+        ups = sum(u for _, u in items)
+        tot = {c: sum(d.get(c, 0.0) for d, _ in items) for c in COUNTERS}
+        wall = sum(d["t"] for d, _ in items)
+        res[key] = {"kernel": items[0][0]["name"], "launches": len(items), "node_updates": ups,
+                    "valu_wave_insts_per_update": tot["SQ_INSTS_VALU"] / ups,
+                    "valu_busy_frac": tot["SQ_ACTIVE_INST_VALU"] / max(tot["SQ_WAVE_CYCLES"], 1),
+                    "effective_clock_GHz": (tot["GRBM_GUI_ACTIVE"] / 8 / wall / 1e9) if wall else None,
+                    "profiled_kernel_s": wall, "counters": tot,
+                    "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
+    doc = {"kernels": res, "valu_peak": "256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s "
+                                        "(MI355X_MICROARCH.md: chip parameters, wave scheduling)"}
+    (ROOT / "gpurun_out" / "r02_valu_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
+    print(json.dumps({k: {kk: v[kk] for kk in ("valu_wave_insts_per_update", "valu_busy_frac", "effective_clock_GHz",
+                                               "launches")} for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
