@@ -15,13 +15,15 @@ its code; under ``torch.distributed.run`` ``--gpus`` must equal ``WORLD_SIZE``. 
 (envs are independent); barrier + max-over-ranks timing; ``n_gpus`` = the process group's size.
 
 Order: the supplementary measurements (rollout, BASELINE config 2, the past-MALL 8M-env
-step run, config 5's R6 chunks with their all-gather) run FIRST, the headline's W warm-up and
-K timed launches after them: at K = 20 the line would otherwise time the GPU's clock ramp
-(9.4 us per launch after 5 warm-up launches, 7.0 us after 5,000). The memory
-floor of the same access pattern (``tools/mall_probe.hip``) is measured right after the timed
-launches, in the same clock state, and is the 1M line's roofline peak (the 32 MiB state stays
-in the Infinity Cache / L2 between launches, and MI355X_MICROARCH.md gives no streaming figure
-for those); the HBM roofline (8 TB/s spec) comes from the 8M-env run (256 MiB of state).
+step run, config 5's R6 chunks with their all-gather) run first, the headline's W warm-up and K
+timed launches after them. The per-launch time depends on where the trajectory is: from fair-bit
+initial states about 40 % of envs change their updated bit per launch and are written back,
+falling to about 9 % after ~1,000 launches -- not a clock ramp. The roofline's
+bytes follow the window actually timed: the changed fraction over exactly the K timed launches
+is measured on a twin batch (same seed: identical Philox trajectory) after the timing. The 1M
+line's state stays in the Infinity Cache (MALL), so its peak is the guide's MALL rate; the HBM
+roofline (8 TB/s spec) comes from the 8M-env run (256 MiB of state). The memory floor of the same
+access pattern (``tools/mall_probe.hip``, no compute) is reported beside each.
 
 Prints ONE JSON line (rank 0) with ``roofline`` and ``cpu_baseline`` (the oracle's C
 restatement on host cores, rank 0 at N = 1 only).
@@ -43,6 +45,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# MI355X_MICROARCH.md "Indexed rows: gather into LDS": rows of a 38 MB table served from the Infinity
+# Cache (MALL) read at 8.6 TB/s chip-wide -- the guide's only MALL rate, used as the 1M line's peak
+MALL_PEAK_GBS = 8600.0
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s
 
 
@@ -141,25 +146,43 @@ class MemFloor:
         return us.value
 
 
-def changed_fraction(batch) -> float:
-    """Fraction of envs whose updated node changed value in one step (the dirty-store kernel
-    writes exactly those envs back): two host copies of the state around one launch."""
-    import numpy as np
+def window_changed_fraction(net, B, device, seed, env_base, warmup, steps):
+    """Mean fraction of envs whose updated node changed value per launch over launches
+    [warmup, warmup + steps) of a batch -- the envs the dirty-store kernel writes back. Measured
+    on a TWIN batch (same network, seed, env ids, fair-bit start: Philox makes its trajectory
+    identical), one launch at a time with the state compared on the device, after the timed run."""
+    import torch
 
-    a = batch.get_state()
-    batch.step(1)
-    b = batch.get_state()
-    return float(np.any(a != b, axis=1).mean())
-
-
-def step_run(net, B, device, seed, warmup, steps, env_base=0):
-    """W + K step launches on a fresh batch; K timed with HIP events on the batch stream."""
     from gym_pbn_amd.batch import PBNBatch
 
     b = PBNBatch(net, B, device=device, seed=seed, env_id_base=env_base)
     b.randomize()
     b.step(warmup)
+    dev = torch.device("cuda", device)
+    x = torch.empty((B, net.n_words), dtype=torch.int64, device=dev)
+    y = torch.empty_like(x)
+    n = torch.zeros((), dtype=torch.int64, device=dev)
+    for _ in range(steps):
+        b.get_state_device(x.data_ptr())
+        b.step(1)
+        b.get_state_device(y.data_ptr())
+        b.sync()
+        n += (x != y).any(dim=1).sum()
+    b.close()
+    return float(n.item()) / (B * steps)
+
+
+def step_run(net, B, device, seed, warmup, steps, env_base=0):
+    """W + K step launches on a fresh batch; K timed with HIP events on the batch stream (the K
+    launches' graph captured beforehand, so the timed call is one graph replay)."""
+    from gym_pbn_amd.batch import PBNBatch
+
+    b = PBNBatch(net, B, device=device, seed=seed, env_id_base=env_base)
+    b.randomize()
+    b.step(warmup)
+    b.prepare_steps(steps)
     b.sync()
+    time.sleep(0.005)  # idle gap: the timed launches are a run of their own in a kernel trace
     b.timing(2)
     b.step(steps)
     b.timing(0)
@@ -167,26 +190,36 @@ def step_run(net, B, device, seed, warmup, steps, env_base=0):
     return b, ms / 1e3 / max(launches, 1)
 
 
+def min_bytes(n_words: int, B: int, q: float) -> float:
+    """Bytes one step launch must move: every env's state read (8W B), the envs whose bit changed
+    written back (8W B each). SURVEY §8(d) prices 16W B per update (every env written): the
+    kernel writes an env only if its updated bit changed, so that figure exceeds what it moves."""
+    return 8.0 * n_words * B * (1.0 + q)
+
+
 def beyond_mall_supplement(net, device, seed, floor):
     """Step mode on 8,388,608 envs on ONE GPU (BASELINE config 4's whole batch): 256 MiB of
     state, as large as the 256 MiB MALL, so every launch streams the state from HBM. Algorithmic
     bytes (64 B per update) / HIP-event kernel time against the 8 TB/s HBM spec."""
-    B = 1 << 23
-    b, s = step_run(net, B, device, seed, 50, 200)
-    frac_dirty = changed_fraction(b)
+    B, W_, K_ = 1 << 23, 50, 200
+    b, s = step_run(net, B, device, seed, W_, K_)
     b.close()
-    alg = 16 * net.n_words * B
+    q = window_changed_fraction(net, B, device, seed, 0, W_, K_)
+    alg = min_bytes(net.n_words, B, q)
+    contract = 16 * net.n_words * B
     out = {"workload": "Bittner-200 step mode, 8,388,608 envs on one GPU (state 256 MiB, past the MALL)",
            "bound": "hbm", "achieved": alg / s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": alg / s / 1e9 / HBM_PEAK_GBS, "avg_kernel_us": s * 1e6, "launches_timed": 200,
-           "alg_bytes_per_launch": alg, "env_steps_per_s": B / s, "changed_env_frac": frac_dirty}
+           "frac": alg / s / 1e9 / HBM_PEAK_GBS, "avg_kernel_us": s * 1e6, "launches_timed": K_,
+           "warmup_launches": W_, "alg_bytes_per_launch": alg, "changed_env_frac": q,
+           "contract_bytes_per_launch": contract, "achieved_at_contract_bytes": contract / s / 1e9,
+           "env_steps_per_s": B / s}
     traffic, src = read_pmc(str(ROOT / "profiles" / "pmc_traffic.json"), f"{net.name}:{B}")
     out["traffic"] = traffic
     if traffic:
         out["traffic_GBs"] = traffic / s / 1e9
         out["traffic_frac"] = traffic / s / 1e9 / HBM_PEAK_GBS
     if floor is not None:
-        fl = floor.us_per_launch(B, round(100 * frac_dirty), 50)
+        fl = floor.us_per_launch(B, round(100 * q), 50)
         out["floor_us"] = fl
         out["frac_of_floor"] = fl / (s * 1e6)
     return out
@@ -454,7 +487,9 @@ def main():
     batch = PBNBatch(net, B, device=device, env_id_base=shard.env_base, seed=args.seed)
     batch.randomize()
     batch.step(args.warmup)
+    batch.prepare_steps(args.steps)  # setup, nothing runs (graph capture where the batch uses graphs)
     batch.sync()
+    time.sleep(0.005)  # idle gap: the timed launches are a run of their own in a kernel trace
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -469,54 +504,62 @@ def main():
     kernel_ms, launches = batch.timing_read()
     elapsed = max_over_ranks(t1 - t0, dist, device=f"cuda:{device}")
     kernel_ms = max_over_ranks(kernel_ms, dist, device=f"cuda:{device}")
-
-    # memory floor of the same pattern, same clock state: one pass over the state per launch,
-    # 32 B read per env, the changed envs' 32 B written back
-    dirty = changed_fraction(batch)
     batch.close()
+
+    # the bytes the timed launches had to move: the fraction of envs written back per launch over
+    # exactly the timed window (twin batch), then the memory floor of that pattern in the same
+    # clock state (32 B read per env, the changed envs' 32 B written back, no compute)
+    q = window_changed_fraction(net, B, device, args.seed, shard.env_base, args.warmup, args.steps) \
+        if rank == 0 else None
     floor_us = None
-    if floor is not None:
+    if floor is not None and q is not None:
         try:
-            floor_us = floor.us_per_launch(B, round(100 * dirty), max(args.steps, 200))
+            floor_us = floor.us_per_launch(B, round(100 * q), max(args.steps, 200))
         except RuntimeError:
             floor_us = None
 
     W = net.n_words
-    alg_bytes = 16 * W * B  # read + write the packed state of every env
+    contract_bytes = 16 * W * B  # read + write the packed state of every env
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
-    achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
     traffic, pmc_src = read_pmc(args.pmc_file, f"{args.network}:{B}")
     total_steps = world * B * args.steps
     value = total_steps / elapsed
     if rank == 0:
-        peak = alg_bytes / (floor_us * 1e-6) / 1e9 if floor_us else None
+        alg_bytes = min_bytes(W, B, q)
+        achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
         rf = {
             "bound": "mall",
             "achieved": achieved,
-            "peak": peak,
+            "peak": MALL_PEAK_GBS,
             "unit": "GB/s",
-            "frac": (achieved / peak) if (achieved and peak) else None,
+            "frac": (achieved / MALL_PEAK_GBS) if achieved else None,
             "traffic": traffic,
             "kernel": f"pbn::k_step<{W},1,1,0,1024> (predictor mix, dirty store, Philox, 1024-thread groups)",
             "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_rule": "8W B read per env + 8W B written per env whose updated bit changed "
+                              "(changed_env_frac, measured over the timed window on a twin batch)",
+            "changed_env_frac": q,
             "avg_kernel_us": avg_kernel_s * 1e6 if launches else None,
             "timing": "HIP events on the batch stream bracketing the K timed launches",
             "residency": "the 32 MiB state stays in the 256 MiB Infinity Cache (MALL) and the XCDs' L2 between "
                          "launches; the HBM-bound figure is hbm_8m",
-            "peak_source": "memory floor measured live right after the timed launches: tools/mall_probe.hip, the "
-                           "same launch shape (1024-thread groups, 2 per CU, env pairs), 32 B read per env and the "
-                           "changed envs' 32 B written back, no compute; peak = alg_bytes / floor time "
-                           "(MI355X_MICROARCH.md gives no Infinity-Cache streaming figure)",
+            "peak_source": "MI355X_MICROARCH.md, Indexed rows: gather into LDS -- a 38 MB table served from the "
+                           "Infinity Cache, 8.6 TB/s chip-wide",
             "floor_us": floor_us,
-            "changed_env_frac": dirty,
-            "frac_of_hbm_spec": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "frac_of_floor": (floor_us / (avg_kernel_s * 1e6)) if (floor_us and launches) else None,
+            "floor_source": "tools/mall_probe.hip run live after the timed launches: the same launch shape "
+                            "(1024-thread groups, 2 per CU, env pairs), 32 B read per env, changed_env_frac of the "
+                            "envs (drawn afresh per launch) written back, no compute",
+            "contract_bytes_per_launch": contract_bytes,
+            "achieved_at_contract_bytes": contract_bytes / avg_kernel_s / 1e9 if launches else None,
             "traffic_source": pmc_src,
             "traffic_GBs": (traffic / avg_kernel_s / 1e9) if (traffic and launches) else None,
         }
         bm = sup.get("beyond_mall_8m")
         if bm and "error" not in bm:
             rf["hbm_8m"] = {k: bm.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                   "traffic_frac", "avg_kernel_us", "floor_us", "frac_of_floor")}
+                                                   "traffic_frac", "avg_kernel_us", "changed_env_frac",
+                                                   "alg_bytes_per_launch", "floor_us", "frac_of_floor")}
         if isinstance(copy, float):
             rf["achievable_copy_GBs"] = copy
             rf["achievable_copy_source"] = "torch device-to-device copy of 2 GiB (past the MALL), read + write bytes"

@@ -140,6 +140,7 @@ struct pbn_envcfg {
 
 constexpr uint32_t STEP_GRAPH_K = 64;  // longest captured run of step launches
 constexpr int STEP_GRAPH_SIZES = 6;     // graphs of 64, 32, 16, 8, 4 and 2 launches
+constexpr uint64_t STEP_GRAPH_MAX_WORDS = 1ull << 20;  // state words from which step mode launches plainly
 
 struct pbn_batch {
     pbn_net* net = nullptr;
@@ -168,12 +169,23 @@ struct pbn_batch {
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
                               // count, -1 = by size
     int roll_group = 1;       // PBNSIM_ROLL_GROUP: lanes per env of the rollout kernel (default by size)
-    bool step_graph_off = false;  // PBNSIM_STEP_GRAPH=0: step mode without HIP graphs
+    // step mode without HIP graphs: by default for large batches (a graph replay's start on the
+    // device costs more than host submission, which a long kernel hides: 1M Bittner-200 envs, 20
+    // launches: 9.3 us per launch plain vs 9.9 us as one replay); PBNSIM_STEP_GRAPH=0/1 forces it
+    bool step_graph_off = false;
     // step_graph[j]: (STEP_GRAPH_K >> j) step launches + k_bump, captured once (all sizes at the
     // first call of two or more steps)
     hipGraphExec_t step_graph[STEP_GRAPH_SIZES] = {};
     bool step_graph_built = false;
     bool step_graph_broken = false;       // capture or instantiation failed once: plain launches
+    // exact-length graphs: one replay for a whole call of n steps (pbn_step_prepare, or the second
+    // call with the same n); each extra replay in a call costs a graph start on the device (~13 us)
+    static constexpr int EXACT_GRAPHS = 4;
+    uint32_t exact_n[EXACT_GRAPHS] = {};
+    hipGraphExec_t exact_graph[EXACT_GRAPHS] = {};
+    uint64_t exact_used[EXACT_GRAPHS] = {};  // LRU stamps
+    uint64_t exact_clock = 0;
+    uint32_t last_step_n = 0;
     DevBuf s_ubase;                       // device copy of update_count for graph replays
     DevBuf s_flip_err;                    // range-error flag of pbn_flip_device
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
@@ -191,6 +203,8 @@ struct pbn_batch {
     size_t ev_used = 0;
     uint64_t region_launches = 0;
     bool region_closed = false;
+    hipEvent_t region_start = nullptr;  // ev_pool[0].first once the region's first launch is queued
+    hipEvent_t region_end = nullptr;    // the closed region's stop event
     int mt_ready = 0;
 
     int grid_for(uint64_t items, int bpc, int block = BLOCK) const {
@@ -210,7 +224,10 @@ struct pbn_batch {
                 HIP_TRY(hipEventCreate(&b));
                 ev_pool.emplace_back(a, b);
             }
-            if (region_launches == 0) HIP_TRY(hipEventRecord(ev_pool[0].first, stream));
+            if (region_launches == 0) {
+                HIP_TRY(hipEventRecord(ev_pool[0].first, stream));
+                region_start = ev_pool[0].first;
+            }
             region_launches++;
             ev_used = 1;
             return 0;  // the stop event is recorded once: pbn_timing_enable(0) or pbn_timing_read
@@ -439,7 +456,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PBN_E_HIP, "hipGetDeviceProperties"));
     b->n_cu = prop.multiProcessorCount;
     if (const char* sbv = getenv("PBNSIM_STEP_BLOCK"))
-        b->step_block = atoi(sbv) == 256 ? 256 : 1024;
+        b->step_block = atoi(sbv) == 256 ? 256 : atoi(sbv) == 512 ? 512 : 1024;
     else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
         b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
@@ -452,6 +469,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
         const int w = atoi(v);
         b->ssd_shared = w == 0 ? 0 : (w == 4 || w == 8) ? w : 1;
     }
+    b->step_graph_off = n_envs * (uint64_t)b->W >= STEP_GRAPH_MAX_WORDS;
     if (const char* v = getenv("PBNSIM_STEP_GRAPH")) b->step_graph_off = atoi(v) == 0;
     // rollout lanes per env: 1 = k_rollout; 2/4/8 = k_rollout_grp (predictor mix, N <= 256)
     b->roll_group = roll_group_size(b, net);
@@ -498,6 +516,8 @@ void pbn_batch_destroy(pbn_batch* b) {
                       &b->s_counter, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase, &b->s_flip_err})
         d->release();
     for (hipGraphExec_t& g : b->step_graph)
+        if (g) (void)hipGraphExecDestroy(g);
+    for (hipGraphExec_t& g : b->exact_graph)
         if (g) (void)hipGraphExecDestroy(g);
     b->pin.release();
     if (b->own_stream) {
@@ -777,15 +797,92 @@ static bool step_graph_ready(pbn_batch* b) {
     return true;
 }
 
+// Captures n step launches + k_bump(n) as one graph in a free (or the least recently used)
+// exact-length slot. Returns the slot, or -1 (plain launches / power-of-two graphs then).
+static int exact_graph_build(pbn_batch* b, uint32_t n) {
+    if (n < 2 || n > PBN_STEP_PREPARE_MAX || b->step_graph_broken || b->step_graph_off || !b->stream) return -1;
+    if (b->s_ubase.ensure(64)) return -1;
+    int slot = 0;
+    for (int j = 1; j < pbn_batch::EXACT_GRAPHS; ++j)
+        if (b->exact_used[j] < b->exact_used[slot]) slot = j;
+    if (b->exact_graph[slot]) {
+        (void)hipGraphExecDestroy(b->exact_graph[slot]);
+        b->exact_graph[slot] = nullptr;
+        b->exact_n[slot] = 0;
+    }
+    // no k_bump: pbn_step writes the device counter before every replay of an exact graph
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    bool launched = ok;
+    for (uint32_t k = 0; launched && k < n; ++k)
+        launched = step_launch(b, 1, k, 0, nullptr, nullptr, (const uint64_t*)b->s_ubase.p, false) == 0;
+    if (ok) ok = hipStreamEndCapture(b->stream, &g) == hipSuccess && launched && g;
+    if (ok) ok = hipGraphInstantiate(&b->exact_graph[slot], g, nullptr, nullptr, 0) == hipSuccess;
+    // upload now, so the first replay (e.g. a timed one) does not pay for it
+    if (ok) ok = hipGraphUpload(b->exact_graph[slot], b->stream) == hipSuccess;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok) {
+        if (b->exact_graph[slot]) (void)hipGraphExecDestroy(b->exact_graph[slot]);
+        b->exact_graph[slot] = nullptr;
+        (void)hipGetLastError();
+        g_err.clear();
+        return -1;
+    }
+    b->exact_n[slot] = n;
+    b->exact_used[slot] = ++b->exact_clock;
+    return slot;
+}
+
+static int exact_graph_find(pbn_batch* b, uint32_t n) {
+    for (int j = 0; j < pbn_batch::EXACT_GRAPHS; ++j)
+        if (b->exact_graph[j] && b->exact_n[j] == n) return j;
+    return -1;
+}
+
+static bool stream_capturing(pbn_batch* b) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (b->stream && hipStreamIsCapturing(b->stream, &cap) != hipSuccess) return true;
+    return cap != hipStreamCaptureStatusNone;
+}
+
+int pbn_step_prepare(pbn_batch* b, uint32_t n_updates) {
+    CHECK_NN(b, "batch");
+    if (n_updates > PBN_STEP_PREPARE_MAX)
+        return fail(PBN_E_INVALID, "n_updates=%u above PBN_STEP_PREPARE_MAX", n_updates);
+    SET_DEV(b);
+    if (n_updates < 2 || b->step_graph_off || stream_capturing(b) || exact_graph_find(b, n_updates) >= 0) return 0;
+    (void)exact_graph_build(b, n_updates);  // on failure pbn_step falls back to plain launches
+    return 0;
+}
+
 int pbn_step(pbn_batch* b, uint32_t n_updates) {
     CHECK_NN(b, "batch");
     SET_DEV(b);
     uint32_t t = 0;
     // not while the caller is capturing the stream into a graph of its own: plain launches then
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (b->stream && hipStreamIsCapturing(b->stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
+    const bool cap = stream_capturing(b);
     const uint32_t smallest = STEP_GRAPH_K >> (STEP_GRAPH_SIZES - 1);
-    if (n_updates >= smallest && b->timing != 1 && cap == hipStreamCaptureStatusNone && step_graph_ready(b)) {
+    int exact = -1;
+    if (!cap && b->timing != 1 && n_updates >= 2 && !b->step_graph_off) {
+        exact = exact_graph_find(b, n_updates);
+        // a length seen twice in a row gets its own graph (an RL loop's fixed step count)
+        if (exact < 0 && n_updates == b->last_step_n) exact = exact_graph_build(b, n_updates);
+    }
+    b->last_step_n = n_updates;
+    if (exact >= 0) {
+        uint32_t* c = (uint32_t*)b->s_ubase.p;
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c, (int)(uint32_t)b->update_count, 1, b->stream));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c + 1), (int)(uint32_t)(b->update_count >> 32), 1, b->stream));
+        hipEvent_t stop;
+        if (int rc = b->ev_begin(&stop)) return rc;
+        if (b->timing == 2) b->region_launches += n_updates - 1;  // ev_begin counted one
+        HIP_TRY(hipGraphLaunch(b->exact_graph[exact], b->stream));
+        if (int rc = b->ev_end(stop)) return rc;
+        b->exact_used[exact] = ++b->exact_clock;
+        b->update_count += n_updates;
+        return 0;
+    }
+    if (n_updates >= smallest && b->timing != 1 && !cap && step_graph_ready(b)) {
         // device counter <- update_count (two 32-bit memsets: stream-ordered, no host buffer)
         uint32_t* c = (uint32_t*)b->s_ubase.p;
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c, (int)(uint32_t)b->update_count, 1, b->stream));
@@ -1362,12 +1459,22 @@ int pbn_env_step_multi_replay(pbn_batch* b, const pbn_envcfg* cfg_c, const int32
 }
 
 // ------------------------------------------------------------------ timing
+// Region timing: the stop event is recorded on the stream now, right behind the last launch.
+static int close_region(pbn_batch* b) {
+    b->region_end = nullptr;
+    if (!b->region_launches) return 0;
+    if (b->ev_pool.empty()) return fail(PBN_E_HIP, "timing region without events");
+    HIP_TRY(hipEventRecord(b->ev_pool[0].second, b->stream));
+    b->region_end = b->ev_pool[0].second;
+    return 0;
+}
+
 int pbn_timing_enable(pbn_batch* b, int enable) {
     CHECK_NN(b, "batch");
     if (enable < 0 || enable > 2) return fail(PBN_E_INVALID, "timing mode must be 0, 1 or 2");
     if (b->timing == 2 && enable != 2) {
         // close the open region right behind the last launch; pbn_timing_read reports it
-        if (b->region_launches) HIP_TRY(hipEventRecord(b->ev_pool[0].second, b->stream));
+        if (int rc = close_region(b)) return rc;
         b->region_closed = true;
         b->timing = enable;
         return 0;
@@ -1376,6 +1483,7 @@ int pbn_timing_enable(pbn_batch* b, int enable) {
     b->ev_used = 0;
     b->region_launches = 0;
     b->region_closed = false;
+    b->region_start = b->region_end = nullptr;
     return 0;
 }
 
@@ -1383,19 +1491,27 @@ int pbn_timing_read(pbn_batch* b, double* kernel_ms, uint64_t* launches) {
     CHECK_NN(b, "batch");
     SET_DEV(b);
     const bool region = b->timing == 2 || b->region_closed;
-    if (b->timing == 2 && b->region_launches) HIP_TRY(hipEventRecord(b->ev_pool[0].second, b->stream));
+    if (b->timing == 2)
+        if (int rc = close_region(b)) return rc;
     HIP_TRY(hipStreamSynchronize(b->stream));
     double tot = 0;
-    for (size_t k = 0; k < b->ev_used; k++) {
+    if (region) {
         float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, b->ev_pool[k].first, b->ev_pool[k].second));
-        tot += ms;
+        if (b->region_launches) HIP_TRY(hipEventElapsedTime(&ms, b->region_start, b->region_end));
+        tot = ms;
+    } else {
+        for (size_t k = 0; k < b->ev_used; k++) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, b->ev_pool[k].first, b->ev_pool[k].second));
+            tot += ms;
+        }
     }
     if (kernel_ms) *kernel_ms = tot;
     if (launches) *launches = region ? b->region_launches : b->ev_used;
     b->ev_used = 0;
     b->region_launches = 0;
     b->region_closed = false;
+    b->region_start = b->region_end = nullptr;
     return 0;
 }
 

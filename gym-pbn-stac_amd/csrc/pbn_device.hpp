@@ -27,8 +27,10 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
         }
         const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        // three-input XOR in one gfx950 v_bitop3_b32 (truth table 0x96), the key from an SGPR;
+        // the compiler only forms a few of these on its own
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(k0, (uint32_t)(p1 >> 32), c[1], 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(k1, (uint32_t)(p0 >> 32), c[3], 0x96);
         c[1] = (uint32_t)p1;
         c[3] = (uint32_t)p0;
         c[0] = n0;
@@ -147,9 +149,27 @@ using Plane = PlaneT<BLOCK>;
 __device__ __forceinline__ uint32_t predictor_choice(uint32_t i, uint64_t k53, const uint8_t* tbl,
                                                      const NetLayout& L) {
     const ulonglong2* thr = reinterpret_cast<const ulonglong2*>(tbl + L.off_thr) + (i * L.tp >> 1);
+    const uint32_t n2 = L.tp >> 1;
     uint32_t j = 0;
+    // up to 8 thresholds (Bittner-200: 4): every read issued before the first compare, so one LDS
+    // round trip; n2 is wave-uniform (scalar branches). Reads past the node's row stay inside the
+    // image / planes and are masked out.
+    if (n2 == 2) {
+        const ulonglong2 t0 = thr[0], t1 = thr[1];
+        return (k53 >= t0.x ? 1u : 0u) + (k53 >= t0.y ? 1u : 0u) + (k53 >= t1.x ? 1u : 0u) +
+               (k53 >= t1.y ? 1u : 0u);
+    }
+    if (n2 <= 4) {
+        ulonglong2 t[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) t[q] = thr[q];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            j += q < n2 ? (k53 >= t[q].x ? 1u : 0u) + (k53 >= t[q].y ? 1u : 0u) : 0u;
+        return j;
+    }
 #pragma unroll 4  // several independent 16-B reads in flight (Bittner-28: 7 per update)
-    for (uint32_t q = 0; q < (L.tp >> 1); ++q) {
+    for (uint32_t q = 0; q < n2; ++q) {
         const ulonglong2 t = thr[q];
         j += (k53 >= t.x ? 1u : 0u) + (k53 >= t.y ? 1u : 0u);
     }

@@ -97,6 +97,7 @@ SIGNATURES = {
     "pbn_flip": (C.c_int, [_vp, _i32p, C.c_int, C.c_int, C.c_int]),
     "pbn_flip_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, C.c_int]),
     "pbn_step": (C.c_int, [_vp, C.c_uint32]),
+    "pbn_step_prepare": (C.c_int, [_vp, C.c_uint32]),
     "pbn_rollout": (C.c_int, [_vp, C.c_uint32]),
     "pbn_step_replay": (C.c_int, [_vp, _u32p, _u64p, C.c_uint32]),
     "pbn_mt_seed": (C.c_int, [_vp, _u64p, C.c_int]),

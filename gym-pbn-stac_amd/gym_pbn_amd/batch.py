@@ -277,6 +277,10 @@ class PBNBatch:
     def step(self, n_updates: int = 1):
         L.check(L.lib.pbn_step(self._h, int(n_updates)))
 
+    def prepare_steps(self, n_updates: int):
+        """Capture the HIP graph for ``step(n_updates)`` now (setup; nothing runs)."""
+        L.check(L.lib.pbn_step_prepare(self._h, int(n_updates)))
+
     def rollout(self, n_updates: int):
         L.check(L.lib.pbn_rollout(self._h, int(n_updates)))
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 9
+#define PBN_ABI_VERSION 10
 
 enum {
     PBN_OK = 0,
@@ -162,10 +162,20 @@ int pbn_flip(pbn_batch *b, const int32_t *actions, int A, int offset, int dedup)
 int pbn_flip_device(pbn_batch *b, const int32_t *d_actions, int A, int offset, int dedup, int check);
 
 /* ---- the hot path: Graph.step (base.py:306-312) / PBN.step (pbn.py:129-133) ---- */
-/* Philox mode, n_updates launches of one update each (state round-trips HBM). Runs of 64
- * launches are replayed from one captured HIP graph (not on the null stream, nor with
- * per-launch timing); results are identical either way. */
+/* Philox mode, n_updates launches of one update each (state round-trips HBM). For batches under
+ * 2^20 state words (launch-bound kernels) calls of two or more launches replay captured HIP graphs
+ * (not on the null stream, nor with per-launch timing): one graph of exactly n_updates launches
+ * when one is cached (pbn_step_prepare, or a call with the same n_updates as the previous call),
+ * otherwise graphs of 64, 32, ..., 2 launches by the binary digits of n_updates. Larger batches
+ * launch plainly (PBNSIM_STEP_GRAPH=0/1 overrides). Results are identical either way. */
 int pbn_step(pbn_batch *b, uint32_t n_updates);
+/* Captures the graph of exactly n_updates step launches now (setup only: nothing runs, the state
+ * is untouched), so that a later pbn_step(b, n_updates) is one graph replay (batches that use
+ * graphs, see pbn_step; a no-op otherwise). The batch keeps the
+ * four most recently used lengths. n_updates < 2 is a no-op; above PBN_STEP_PREPARE_MAX,
+ * PBN_E_INVALID. A failed capture is not an error (pbn_step then launches without it). */
+#define PBN_STEP_PREPARE_MAX 4096
+int pbn_step_prepare(pbn_batch *b, uint32_t n_updates);
 /* Philox mode, one launch applying n_updates in registers; bit-identical to pbn_step. */
 int pbn_rollout(pbn_batch *b, uint32_t n_updates);
 /* Replay mode: node_idx [T][B] (randint result) and k53 [T][B] (random() * 2^53), host arrays. */

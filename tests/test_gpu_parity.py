@@ -107,6 +107,42 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
     b.close()
 
 
+def test_exact_length_step_graphs_match_oracle(G, oracle_mod):
+    """pbn_step_prepare(n) captures one graph of exactly n launches without running anything; a
+    length called twice in a row gets one too; the batch keeps four lengths (least recently used
+    evicted). Every replay continues the update counter exactly."""
+    net = load_network("bittner199")
+    o = oracle_mod.Oracle(net)
+    b = G.PBNBatch(net, 4099, seed=19, env_id_base=7)
+    b.randomize()
+    init = b.get_state()
+    b.prepare_steps(20)
+    b.prepare_steps(1)  # no-op
+    assert np.array_equal(b.get_state(), init)  # setup only
+    done = 0
+    for n in (20, 20, 7, 7, 7, 33, 33, 5, 5, 9, 9, 20, 3, 20):  # 5 lengths through 4 slots
+        b.timing(2)
+        b.step(n)
+        b.timing(0)
+        ms, launches = b.timing_read()
+        assert launches == n and ms > 0
+        done += n
+        assert np.array_equal(b.get_state(), o.step_philox(init, 19, 7, 0, done)), n
+    b.timing(2)  # a region mixing an exact graph with plain launches and other graphs
+    b.step(20)
+    b.step(1)
+    b.step(20)
+    b.rollout(3)
+    b.timing(0)
+    ms, launches = b.timing_read()
+    assert launches == 42 and ms > 0  # 41 step launches + one rollout launch (3 updates)
+    done += 44
+    assert np.array_equal(b.get_state(), o.step_philox(init, 19, 7, 0, done))
+    with pytest.raises(Exception):
+        b.prepare_steps(4097)
+    b.close()
+
+
 def test_step_inside_a_torch_graph_capture(G, oracle_mod):
     """pbn_step on a stream the caller is capturing (torch.cuda.graph) launches plainly into the
     caller's graph instead of capturing one of its own; replaying the caller's graph repeats the

@@ -16,7 +16,8 @@
 namespace {
 
 __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64_t B, uint32_t write_pct,
-                                                uint32_t passes, uint64_t* __restrict__ sink) {
+                                                uint32_t passes, uint64_t* __restrict__ sink, uint32_t salt,
+                                                uint32_t glog) {
     const uint64_t stride = (uint64_t)gridDim.x * 1024u;
     uint64_t acc = 0;
     for (uint32_t p = 0; p < passes; ++p) {
@@ -36,14 +37,14 @@ __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64
             acc ^= a0.x ^ a1.y;
             // a fixed subset of envs is written (write_pct %), as the dirty-store kernel writes
             // the envs whose updated bit changed
-            if ((uint32_t)((ea * 2654435761u) >> 7) % 100u < write_pct) {
+            if ((uint32_t)((((ea >> glog) ^ salt) * 2654435761u) >> 7) % 100u < write_pct) {
                 a0.x += 1;
                 qa[0] = a0;
                 qa[1] = a1;
             }
             if (hb) {
                 acc ^= b0.x ^ b1.y;
-                if ((uint32_t)((eb * 2654435761u) >> 7) % 100u < write_pct) {
+                if ((uint32_t)((((eb >> glog) ^ salt) * 2654435761u) >> 7) % 100u < write_pct) {
                     b0.x += 1;
                     qb[0] = b0;
                     qb[1] = b1;
@@ -59,7 +60,8 @@ __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64
 // Average time per PASS over the state (microseconds) for n_envs 32-B envs, the given write
 // fraction, `passes` passes per launch and `launches` timed launches (after 3 untimed ones).
 // Returns 0 on success, a HIP error code otherwise.
-extern "C" int mall_probe(uint64_t n_envs, int write_pct, int passes, int launches, double* us_per_pass) {
+static int probe_impl(uint64_t n_envs, int write_pct, int passes, int launches, int vary, int glog,
+                      double* us_per_pass) {
     if (!us_per_pass || n_envs < 2048 || passes < 1 || launches < 1) return -1;
     int dev = 0, n_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -2;
@@ -77,13 +79,15 @@ extern "C" int mall_probe(uint64_t n_envs, int write_pct, int passes, int launch
     const int grid = (int)(want < (uint64_t)n_cu * 2u ? want : (uint64_t)n_cu * 2u);
     if (e == hipSuccess) {
         for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(k_probe, dim3(grid), dim3(1024), 0, 0, s, n_envs,
-                                                       (uint32_t)write_pct, (uint32_t)passes, sink);
+                                                       (uint32_t)write_pct, (uint32_t)passes, sink,
+                                                       vary ? (uint32_t)(w * 0x9E3779B1u) : 0u, (uint32_t)glog);
         e = hipEventRecord(t0, 0);
     }
     if (e == hipSuccess) {
         for (int k = 0; k < launches; ++k)
             hipLaunchKernelGGL(k_probe, dim3(grid), dim3(1024), 0, 0, s, n_envs, (uint32_t)write_pct,
-                               (uint32_t)passes, sink);
+                               (uint32_t)passes, sink, vary ? (uint32_t)((k + 3) * 0x9E3779B1u) : 0u,
+                               (uint32_t)glog);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipEventRecord(t1, 0);
@@ -96,4 +100,18 @@ extern "C" int mall_probe(uint64_t n_envs, int write_pct, int passes, int launch
     if (s) (void)hipFree(s);
     if (sink) (void)hipFree(sink);
     return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int mall_probe(uint64_t n_envs, int write_pct, int passes, int launches, double* us_per_pass) {
+    return probe_impl(n_envs, write_pct, passes, launches, 0, 0, us_per_pass);
+}
+
+// The same with the written subset drawn afresh every launch (as the step kernel's changed envs are).
+extern "C" int mall_probe_vary(uint64_t n_envs, int write_pct, int passes, int launches, double* us_per_pass) {
+    return probe_impl(n_envs, write_pct, passes, launches, 1, 0, us_per_pass);
+}
+
+// Written envs decided per aligned group of 2^glog envs (all or none), drawn afresh per launch.
+extern "C" int mall_probe_group(uint64_t n_envs, int write_pct, int glog, int launches, double* us_per_pass) {
+    return probe_impl(n_envs, write_pct, 1, launches, 1, glog, us_per_pass);
 }
