@@ -106,6 +106,7 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             uint64_t(&s)[W] = h ? nxt : cur;
             const uint32_t i = h ? i1 : i0;
             const uint32_t d = i >> 5, sh = i & 31u;
+#ifndef PBN_EXP_NOAPPLY  // measurement builds only: the state consumed without the plane / apply
             to_plane<W>(P, s);
             const uint32_t self = P.get(d);
             uint32_t y;
@@ -113,6 +114,10 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
                 y = predictor_apply(P, i, self, h ? r1 : r0);
             else
                 y = table_eval_lds(P, i, h ? q1 : q0, lds, a.L);
+#else
+            const uint32_t self = (uint32_t)s[0] ^ (uint32_t)s[W - 1];
+            const uint32_t y = ((self ^ (uint32_t)(h ? r1 : r0)) >> sh) & 1u;
+#endif
             const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
             if constexpr (STORE == STORE_DIRTY) {
                 // store the whole env (32 B at W = 4), and only if its bit changed: a full
@@ -556,17 +561,25 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             // chain is its state-plane read (every entry of the chunk was generated for this lane).
             bool act = true;
             uint32_t e1 = gbuf[lane];  // entry of update c + 1 (record and delta loaded)
-            uint64_t r1 = recs[(e1 & 0x1FFu) * a.L.pmax + (e1 >> 9)];
+            uint64_t r1 = recs[__umul24(e1 & 0x1FFu, a.L.pmax) + (e1 >> 9)];
             uint2 n1 = ndelta[e1 & 0x1FFu];
             uint32_t e2 = gbuf[64 + lane];  // entry of update c + 2
-            static_assert(ENV_CHUNK >= 2, "prefetch depth");
-            for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
+            static_assert(ENV_CHUNK >= 2 && ENV_CHUNK % ENV_UNROLL == 0, "prefetch depth / unroll");
+            // the wave tests for "no lane active" once per ENV_UNROLL updates, not per update: the
+            // per-update ballot + branch made every update wait for the whole previous one (the
+            // wave cannot issue past an unresolved branch), so the state chain of update c + 1
+            // could not overlap the counters / attractor test of update c. Lanes that finish
+            // inside a block run its remaining updates masked (act = 0: nothing is written).
+            for (uint32_t c0 = 0; c0 < ENV_CHUNK; c0 += ENV_UNROLL) {
+#pragma unroll
+            for (uint32_t u = 0; u < ENV_UNROLL; ++u) {
+                const uint32_t c = c0 + u;
                 const uint32_t ent = e1;
                 const uint64_t rec = r1;
                 const uint2 nd = n1;
                 // unconditional (clamped) prefetches: no branch, so no wait before the plane reads
                 e1 = e2;
-                r1 = recs[(e1 & 0x1FFu) * a.L.pmax + (e1 >> 9)];
+                r1 = recs[__umul24(e1 & 0x1FFu, a.L.pmax) + (e1 >> 9)];
                 n1 = ndelta[e1 & 0x1FFu];
                 e2 = gbuf[min(c + 2, ENV_CHUNK - 1) * 64 + lane];
                 const bool cap_now = used >= a.update_cap;
@@ -586,7 +599,8 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 const bool hz = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
                 const bool hit = act & (((used == 1) & !a.first_tested) ? hit0 : hz);
                 act = act & !hit;
-                if (__ballot(act) == 0) break;
+            }
+            if (__ballot(act) == 0) break;
             }
             done = !act;
         } else

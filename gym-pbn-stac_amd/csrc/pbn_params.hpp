@@ -184,6 +184,10 @@ uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp);
 #define PBN_ENV_CHUNK 32
 #endif
 constexpr uint32_t ENV_CHUNK = PBN_ENV_CHUNK;  // updates per lane between refill rounds
+#ifndef PBN_ENV_UNROLL
+#define PBN_ENV_UNROLL 8
+#endif
+constexpr uint32_t ENV_UNROLL = PBN_ENV_UNROLL;  // updates between the wave's "any lane active" tests
 constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
