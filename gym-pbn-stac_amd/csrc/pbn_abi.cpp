@@ -456,7 +456,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PBN_E_HIP, "hipGetDeviceProperties"));
     b->n_cu = prop.multiProcessorCount;
     if (const char* sbv = getenv("PBNSIM_STEP_BLOCK"))
-        b->step_block = atoi(sbv) == 256 ? 256 : atoi(sbv) == 512 ? 512 : 1024;
+        b->step_block = atoi(sbv) == 256 ? 256 : 1024;
     else  // 1024-thread groups stage the image 4x less often; small batches need more, smaller groups
         b->step_block = n_envs >= (uint64_t)b->n_cu * 1024u * (uint64_t)b->envs_per_thread ? 1024 : 256;
     b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
@@ -800,7 +800,7 @@ static bool step_graph_ready(pbn_batch* b) {
 // Captures n step launches + k_bump(n) as one graph in a free (or the least recently used)
 // exact-length slot. Returns the slot, or -1 (plain launches / power-of-two graphs then).
 static int exact_graph_build(pbn_batch* b, uint32_t n) {
-    if (n < 2 || n > PBN_STEP_PREPARE_MAX || b->step_graph_broken || b->step_graph_off || !b->stream) return -1;
+    if (n < 2 || n > STEP_GRAPH_K || b->step_graph_broken || b->step_graph_off || !b->stream) return -1;
     if (b->s_ubase.ensure(64)) return -1;
     int slot = 0;
     for (int j = 1; j < pbn_batch::EXACT_GRAPHS; ++j)
@@ -850,8 +850,12 @@ int pbn_step_prepare(pbn_batch* b, uint32_t n_updates) {
     if (n_updates > PBN_STEP_PREPARE_MAX)
         return fail(PBN_E_INVALID, "n_updates=%u above PBN_STEP_PREPARE_MAX", n_updates);
     SET_DEV(b);
-    if (n_updates < 2 || b->step_graph_off || stream_capturing(b) || exact_graph_find(b, n_updates) >= 0) return 0;
-    (void)exact_graph_build(b, n_updates);  // on failure pbn_step falls back to plain launches
+    if (n_updates < 2 || b->step_graph_off || stream_capturing(b)) return 0;
+    // on failure pbn_step falls back to plain launches; runs longer than STEP_GRAPH_K replay the
+    // power-of-two graphs (one graph of thousands of launches replayed slower: 3.43 vs 3.16 us per
+    // launch at 65,536 Bittner-28 envs)
+    if (n_updates > STEP_GRAPH_K) (void)step_graph_ready(b);
+    else if (exact_graph_find(b, n_updates) < 0) (void)exact_graph_build(b, n_updates);
     return 0;
 }
 
@@ -866,7 +870,8 @@ int pbn_step(pbn_batch* b, uint32_t n_updates) {
     if (!cap && b->timing != 1 && n_updates >= 2 && !b->step_graph_off) {
         exact = exact_graph_find(b, n_updates);
         // a length seen twice in a row gets its own graph (an RL loop's fixed step count)
-        if (exact < 0 && n_updates == b->last_step_n) exact = exact_graph_build(b, n_updates);
+        if (exact < 0 && n_updates == b->last_step_n && n_updates <= STEP_GRAPH_K)
+            exact = exact_graph_build(b, n_updates);
     }
     b->last_step_n = n_updates;
     if (exact >= 0) {

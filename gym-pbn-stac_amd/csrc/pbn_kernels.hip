@@ -43,30 +43,11 @@ namespace pbn {
 // they are computed while the pair's state loads are in flight.
 template <int W, int KIND, int STORE, int SB>
 __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, uint64_t e, uint64_t stride,
-                                              uint32_t N) {
+                                              uint64_t (&cur)[W], uint32_t N) {
     // graph replays read the batch's update counter from device memory (k_bump advances it)
     const uint64_t u = a.update_base + (a.ubase_dev ? *a.ubase_dev : 0ull);
     const uint64_t po = stride;  // second env of the pair (adjacent envs measured slower: 8.2 vs 7.8 us)
-    // The image granules are this wave's FIRST loads: loads complete in order, so writing them to
-    // LDS waits for them alone, and the barrier and the predictor choices run while the state
-    // loads issued after them are still in flight.
-    constexpr uint32_t GR = SB >= 1024 ? 1 : 2;  // granules per thread held in registers
-    const uint32_t n16 = a.L.bytes / 16;
-    const uint4* img = reinterpret_cast<const uint4*>(a.img);
-    uint4 gv[GR];
-#pragma unroll
-    for (uint32_t r = 0; r < GR; ++r) {  // unconditional (clamped): no branch around the loads
-        const uint32_t k = threadIdx.x + r * SB;
-#ifndef PBN_EXP_NOSTAGE  // measurement builds only: an all-zero image written from registers
-        gv[r] = img[k < n16 ? k : n16 - 1];
-#else
-        gv[r] = make_uint4(0u, 0u, 0u, (uint32_t)(a.B >> 40));
-#endif
-    }
-    // state loads unconditional too (an env past the batch loads the last env and is never
-    // stored): with no branch around any load the wait for the image counts exactly
-    uint64_t cur[W], nxt[W];
-    load_state<W>(a.state + min(e, a.B - 1) * W, cur);
+    uint64_t nxt[W];
     uint32_t i0 = 0, i1 = 0;
     uint64_t q0 = 0, q1 = 0;
     auto draws = [&](uint64_t ea) {
@@ -78,18 +59,9 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
         q0 = k53_of(w0[1], w0[2]);
         q1 = k53_of(w1[1], w1[2]);
     };
-    load_state<W>(a.state + min(e + po, a.B - 1) * W, nxt);
+    if (e + po < a.B) load_state<W>(a.state + (e + po) * W, nxt);
     draws(e);
-    // the draws are materialised here, before the image is written and the barrier: without this
-    // the compiler sinks Philox behind the barrier, i.e. behind the state loads
-    asm volatile("" ::"v"(i0), "v"(i1), "v"(q0), "v"(q1) : "memory");
-    uint4* limg = reinterpret_cast<uint4*>(lds);
-#pragma unroll
-    for (uint32_t r = 0; r < GR; ++r) {
-        const uint32_t k = threadIdx.x + r * SB;
-        if (k < n16) limg[k] = gv[r];
-    }
-    for (uint32_t k = threadIdx.x + GR * SB; k < n16; k += SB) limg[k] = img[k];  // larger images
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     while (e < a.B) {
@@ -106,7 +78,6 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             uint64_t(&s)[W] = h ? nxt : cur;
             const uint32_t i = h ? i1 : i0;
             const uint32_t d = i >> 5, sh = i & 31u;
-#ifndef PBN_EXP_NOAPPLY  // measurement builds only: the state consumed without the plane / apply
             to_plane<W>(P, s);
             const uint32_t self = P.get(d);
             uint32_t y;
@@ -114,24 +85,20 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
                 y = predictor_apply(P, i, self, h ? r1 : r0);
             else
                 y = table_eval_lds(P, i, h ? q1 : q0, lds, a.L);
-#else
-            const uint32_t self = (uint32_t)s[0] ^ (uint32_t)s[W - 1];
-            const uint32_t y = ((self ^ (uint32_t)(h ? r1 : r0)) >> sh) & 1u;
-#endif
             const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
             if constexpr (STORE == STORE_DIRTY) {
                 // store the whole env (32 B at W = 4), and only if its bit changed: a full
                 // aligned env write measured faster than writing just the 16-B half that holds
                 // node i (7.69 vs 7.93 us at 1M envs), partial sector writes cost extra
                 if (nv != self) {
-                    P.put(d, nv);
+                    // the env's words are still in registers: flip bit i there (one 64-bit select
+                    // per word) rather than writing the plane and reading all 2W dwords back
                     uint64_t out[W];
-                    from_plane<W>(P, out);
-#ifndef PBN_EXP_NOSTORE  // measurement builds only (tools/build_exp.sh): the kernel without its stores
+                    const uint32_t wi = i >> 6;
+                    const uint64_t m = 1ull << (i & 63u);
+#pragma unroll
+                    for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
                     store_state<W>(a.state + eh * W, out);
-#else
-                    if (out[0] == 0x9E3779B97F4A7C15ull) store_state<W>(a.state + eh * W, out);
-#endif
                 }
             } else {
                 P.put(d, nv);
@@ -159,13 +126,13 @@ __global__ __launch_bounds__(SB) void k_step(StepArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * SB;
     uint64_t e = (uint64_t)blockIdx.x * SB + threadIdx.x;
     const uint32_t N = (uint32_t)a.L.n_nodes;
+    uint64_t cur[W];
+    if (e < a.B) load_state<W>(a.state + e * W, cur);
     if constexpr (!REPLAY) {
         // Step mode: the draws depend on (seed, update counter, env id) only, so every
         // draw this thread needs is computed while its state loads are in flight.
-        k_step_single<W, KIND, STORE, SB>(a, lds, e, stride, N);
+        k_step_single<W, KIND, STORE, SB>(a, lds, e, stride, cur, N);
     } else {
-        uint64_t cur[W];
-        if (e < a.B) load_state<W>(a.state + e * W, cur);
         stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
         __syncthreads();
         const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
@@ -1113,7 +1080,6 @@ static void* step_fn(int store, int replay, int sb, int rollout, int grp) {
     if (sb == 1024)
         return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0, 1024>
                                     : (void*)k_step<W, KIND, STORE_FULL, 0, 1024>;
-    if (sb == 512 && store == STORE_DIRTY) return (void*)k_step<W, KIND, STORE_DIRTY, 0, 512>;
     return store == STORE_DIRTY ? (void*)k_step<W, KIND, STORE_DIRTY, 0, BLOCK>
                                 : (void*)k_step<W, KIND, STORE_FULL, 0, BLOCK>;
 }
@@ -1300,7 +1266,7 @@ static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
 
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout, int grp) {
     if (grp > 1) sb = BLOCK;
-    void* fn = step_kernel(W, kind, sb == 512 ? STORE_DIRTY : STORE_FULL, 0, sb, rollout, grp);
+    void* fn = step_kernel(W, kind, STORE_FULL, 0, sb, rollout, grp);
     if (!fn) return (int)hipErrorInvalidValue;
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb, grp), blocks_per_cu);
 }

@@ -164,15 +164,15 @@ int pbn_flip_device(pbn_batch *b, const int32_t *d_actions, int A, int offset, i
 /* ---- the hot path: Graph.step (base.py:306-312) / PBN.step (pbn.py:129-133) ---- */
 /* Philox mode, n_updates launches of one update each (state round-trips HBM). For batches under
  * 2^20 state words (launch-bound kernels) calls of two or more launches replay captured HIP graphs
- * (not on the null stream, nor with per-launch timing): one graph of exactly n_updates launches
- * when one is cached (pbn_step_prepare, or a call with the same n_updates as the previous call),
- * otherwise graphs of 64, 32, ..., 2 launches by the binary digits of n_updates. Larger batches
+ * (not on the null stream, nor with per-launch timing): one graph of exactly n_updates (<= 64)
+ * launches when one is cached (pbn_step_prepare, or a call with the same n_updates as the previous
+ * call), otherwise graphs of 64, 32, ..., 2 launches by the binary digits of n_updates. Larger batches
  * launch plainly (PBNSIM_STEP_GRAPH=0/1 overrides). Results are identical either way. */
 int pbn_step(pbn_batch *b, uint32_t n_updates);
-/* Captures the graph of exactly n_updates step launches now (setup only: nothing runs, the state
- * is untouched), so that a later pbn_step(b, n_updates) is one graph replay (batches that use
- * graphs, see pbn_step; a no-op otherwise). The batch keeps the
- * four most recently used lengths. n_updates < 2 is a no-op; above PBN_STEP_PREPARE_MAX,
+/* Captures the graphs pbn_step(b, n_updates) will replay now (setup only: nothing runs, the state
+ * is untouched): for n_updates <= 64 one graph of exactly that many launches (the batch keeps the
+ * four most recently used lengths), above that the 64, 32, ..., 2-launch graphs. Batches that
+ * launch plainly (see pbn_step): a no-op. n_updates < 2 is a no-op; above PBN_STEP_PREPARE_MAX,
  * PBN_E_INVALID. A failed capture is not an error (pbn_step then launches without it). */
 #define PBN_STEP_PREPARE_MAX 4096
 int pbn_step_prepare(pbn_batch *b, uint32_t n_updates);

@@ -138,6 +138,10 @@ def test_exact_length_step_graphs_match_oracle(G, oracle_mod):
     assert launches == 42 and ms > 0  # 41 step launches + one rollout launch (3 updates)
     done += 44
     assert np.array_equal(b.get_state(), o.step_philox(init, 19, 7, 0, done))
+    b.prepare_steps(200)  # above 64: the power-of-two graphs
+    b.step(200)
+    done += 200
+    assert np.array_equal(b.get_state(), o.step_philox(init, 19, 7, 0, done))
     with pytest.raises(Exception):
         b.prepare_steps(4097)
     b.close()
