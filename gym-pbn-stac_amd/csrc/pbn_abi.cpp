@@ -1277,8 +1277,19 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         if (grp != 2 && grp != 4 && grp != 8) grp = 1;
         if (grp > 1) mode = 3;
     }
+    // cooperative-draw mode keeps 16-B env records in LDS where the 8-B predictor records were
+    // (pbn_device.hpp env_record): the tables after them move up by erec_shift
+    uint32_t erec_shift = 0;
+    if (mode == 2) {
+        const uint32_t nrec = (uint32_t)b->net->N * cfg->L.pmax;
+        erec_shift = cfg->L.off_rec + 16u * nrec - cfg->off_cubes;
+        if (nrec > 65535u || env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1) > 64u * 1024u) {
+            mode = cfg->fast;  // too large for the u16 record index / one workgroup's LDS
+            erec_shift = 0;
+        }
+    }
     int bpc = 1;
-    if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes, &bpc))
+    if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
     if (b->env_bpc) bpc = std::min(bpc, b->env_bpc);
     EnvArgs a{};
@@ -1292,12 +1303,13 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.error = b->d_error;
     a.img = dv->image;
     a.L = cfg->L;
-    a.off_cubes = cfg->off_cubes;
-    a.off_target = cfg->off_target;
-    a.off_ndelta = cfg->off_ndelta;
+    a.off_cubes = cfg->off_cubes + erec_shift;
+    a.off_target = cfg->off_target + erec_shift;
+    a.off_ndelta = cfg->off_ndelta + erec_shift;
+    a.erec_shift = erec_shift;
     a.fast = mode;
     a.grp = grp;
-    a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + 8u * (uint32_t)b->W * BLOCK;
+    a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + erec_shift + 8u * (uint32_t)b->W * BLOCK;
     if (int rc = b->s_counter.ensure(8)) return rc;
     a.counter = (unsigned long long*)b->s_counter.p;
     a.n_cubes = cfg->H;

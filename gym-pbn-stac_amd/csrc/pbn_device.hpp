@@ -209,6 +209,20 @@ __device__ __forceinline__ uint32_t table_eval_lds(const P_t& P, uint32_t i, uin
     return k53 < t ? 1u : 0u;
 }
 
+// Env record (k_env, cooperative-draw mode): predictor record rec (in0 | in1<<16 | in2<<32 | tt<<48)
+// of node i re-encoded for the LDS state planes of 256-lane workgroups: byte offsets of the plane
+// dwords holding in0 / in1 (x), in2 / node i (y), the bit positions in those dwords (z, one byte
+// each: in0, in1, in2, i), tt | i << 16 (w). An update then reads its four plane dwords with no
+// index arithmetic. Inputs are < 512 (W <= 8), so every offset is < 16 KiB.
+__device__ __forceinline__ uint4 env_record(uint64_t rec, uint32_t i) {
+    const uint32_t x0 = (uint32_t)rec & 0xFFFFu, x1 = (uint32_t)(rec >> 16) & 0xFFFFu,
+                   x2 = (uint32_t)(rec >> 32) & 0xFFFFu;
+    auto off = [](uint32_t x) { return (x >> 5) * (uint32_t)(BLOCK * 4); };
+    return make_uint4(off(x0) | (off(x1) << 16), off(x2) | (off(i) << 16),
+                      (x0 & 31u) | ((x1 & 31u) << 8) | ((x2 & 31u) << 16) | ((i & 31u) << 24),
+                      (uint32_t)(rec >> 48) | (i << 16));
+}
+
 // Async update of node i in place on the plane; returns 1 if the bit changed.
 template <class P_t>
 __device__ __forceinline__ uint32_t predictor_update_lds(const P_t& P, uint32_t i, uint64_t k53,

@@ -366,10 +366,25 @@ template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     static_assert(FAST != 2 || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
     extern __shared__ __align__(16) uint8_t lds[];
-    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
-    __syncthreads();
-    const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     const uint32_t N = (uint32_t)a.L.n_nodes;
+    if constexpr (FAST == 2) {
+        // LDS: the thresholds as staged; in place of the 8-B predictor records, 16-B "env
+        // records" (EnvRec) carrying each input's plane offset and bit position, so an update
+        // does no index arithmetic; the cubes / target / deltas after them move up by erec_shift
+        const uint4* g = reinterpret_cast<const uint4*>(a.img);
+        uint4* l = reinterpret_cast<uint4*>(lds);
+        for (uint32_t k = threadIdx.x; k < a.L.off_rec / 16; k += BLOCK) l[k] = g[k];
+        const uint32_t tail = a.off_cubes - a.erec_shift;  // the cubes' offset in the device image
+        for (uint32_t k = threadIdx.x; k < (a.L.bytes - tail) / 16; k += BLOCK)
+            l[(tail + a.erec_shift) / 16 + k] = g[tail / 16 + k];
+        const uint64_t* grec = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(a.img) + a.L.off_rec);
+        uint4* erec = reinterpret_cast<uint4*>(lds + a.L.off_rec);
+        for (uint32_t r = threadIdx.x; r < N * a.L.pmax; r += BLOCK) erec[r] = env_record(grec[r], r / a.L.pmax);
+    } else {
+        stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    }
+    __syncthreads();
+    const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes + a.erec_shift) + threadIdx.x};
     const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
     const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
     const uint2* ndelta = reinterpret_cast<const uint2*>(lds + a.off_ndelta);
@@ -481,7 +496,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                     philox_draw(a.seed, used + sl, a.call_idx + t, gid, STREAM_ENV, w);
                     const uint32_t i = philox_node<KIND>(w[0], N);
                     const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
-                    gbuf[sl * 64 + lane] = (uint16_t)(i | (j << 9));
+                    gbuf[sl * 64 + lane] = (uint16_t)(__umul24(i, a.L.pmax) + j);  // EnvRec index
                 }
             } else {
             if (e >= 0) {
@@ -506,7 +521,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                     philox_draw(a.seed, used_tab[q] + sl, call_tab[q], gid_tab[q], STREAM_ENV, w);
                     const uint32_t i = philox_node<KIND>(w[0], N);
                     const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
-                    gbuf[sl * 64 + q] = (uint16_t)(i | (j << 9));
+                    gbuf[sl * 64 + q] = (uint16_t)(__umul24(i, a.L.pmax) + j);
                 }
             }
             }
@@ -520,18 +535,20 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         const uint64_t g = a.env_base + (uint64_t)e;
         bool done = false;
         if constexpr (FAST == 2) {
-            const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+            const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
+            const uint8_t* pb = reinterpret_cast<const uint8_t*>(P.base);  // this lane's plane column
             // branch-free per lane: a lane that is done keeps iterating masked (no break, so
-            // no per-lane exit bookkeeping); the wave leaves the chunk when no lane is active
-            // The entries, records and counter deltas do not depend on the state: they are read
-            // one and two updates ahead, so an update's only LDS round trip on the dependent
-            // chain is its state-plane read (every entry of the chunk was generated for this lane).
-            bool act = true;
-            uint32_t e1 = gbuf[lane];  // entry of update c + 1 (record and delta loaded)
-            uint64_t r1 = recs[__umul24(e1 & 0x1FFu, a.L.pmax) + (e1 >> 9)];
-            uint2 n1 = ndelta[e1 & 0x1FFu];
-            uint32_t e2 = gbuf[64 + lane];  // entry of update c + 2
-            static_assert(ENV_CHUNK >= 2 && ENV_CHUNK % ENV_UNROLL == 0, "prefetch depth / unroll");
+            // no per-lane exit bookkeeping); the wave leaves the chunk when no lane is active.
+            // Entries, records and counter deltas do not depend on the state: the entry is read
+            // three updates ahead, its EnvRec two ahead and the node's counter deltas one ahead, so
+            // an update's only LDS round trip on the dependent chain is its state-plane read.
+            bool act = true, hitf = false;
+            const uint32_t lim = a.update_cap > used ? a.update_cap - used : 0u;  // updates left
+            uint4 q0 = erec[gbuf[lane]];
+            uint4 q1 = erec[gbuf[64 + lane]];
+            uint2 n0 = ndelta[q0.w >> 16];
+            uint32_t e2 = gbuf[128 + lane];
+            static_assert(ENV_CHUNK >= 3 && ENV_CHUNK % ENV_UNROLL == 0, "prefetch depth / unroll");
             // the wave tests for "no lane active" once per ENV_UNROLL updates, not per update: the
             // per-update ballot + branch made every update wait for the whole previous one (the
             // wave cannot issue past an unresolved branch), so the state chain of update c + 1
@@ -541,34 +558,41 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
             for (uint32_t u = 0; u < ENV_UNROLL; ++u) {
                 const uint32_t c = c0 + u;
-                const uint32_t ent = e1;
-                const uint64_t rec = r1;
-                const uint2 nd = n1;
+                const uint4 q = q0;
+                const uint2 nd = n0;
                 // unconditional (clamped) prefetches: no branch, so no wait before the plane reads
-                e1 = e2;
-                r1 = recs[__umul24(e1 & 0x1FFu, a.L.pmax) + (e1 >> 9)];
-                n1 = ndelta[e1 & 0x1FFu];
-                e2 = gbuf[min(c + 2, ENV_CHUNK - 1) * 64 + lane];
-                const bool cap_now = used >= a.update_cap;
-                capped |= act && cap_now;
-                act = act && !cap_now;
-                const uint32_t i = ent & 0x1FFu;
-                const uint32_t d = i >> 5, sh = i & 31u;
-                const uint32_t self = P.get(d);
-                const uint32_t y = predictor_apply(P, i, self, rec);
-                const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-                P.put(d, act ? nv : self);
+                n0 = ndelta[q1.w >> 16];
+                q0 = q1;
+                q1 = erec[e2];
+                e2 = gbuf[min(c + 3, ENV_CHUNK - 1) * 64 + lane];
+                act = act & (c < lim);  // the update cap (pbn_target_multi.py's loop is unbounded)
+                // Predstep (base.py:100-118): Y = tt[x_in0 x_in1 x_in2 x_self] from the plane
+                const uint32_t b0 = *reinterpret_cast<const uint32_t*>(pb + (q.x & 0xFFFFu));
+                const uint32_t b1 = *reinterpret_cast<const uint32_t*>(pb + (q.x >> 16));
+                const uint32_t b2 = *reinterpret_cast<const uint32_t*>(pb + (q.y & 0xFFFFu));
+                const uint32_t self = *reinterpret_cast<const uint32_t*>(pb + (q.y >> 16));
+                const uint32_t shs = q.z >> 24;
+                const uint32_t xs = __builtin_amdgcn_ubfe(self, shs, 1);
+                const uint32_t p = (__builtin_amdgcn_ubfe(b0, q.z, 1) << 3) |
+                                   (__builtin_amdgcn_ubfe(b1, q.z >> 8, 1) << 2) |
+                                   (__builtin_amdgcn_ubfe(b2, q.z >> 16, 1) << 1) | xs;
+                const uint32_t y = __builtin_amdgcn_ubfe(q.w, p, 1);
+                const uint32_t fl = (xs ^ y) & (act ? 1u : 0u);  // the bit changes (and is applied)
+                *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(pb) + (q.y >> 16)) = self ^ (fl << shs);
                 used += act ? 1u : 0u;
-                const bool changed = act & (nv != self);
-                m_lo += changed ? (y ? nd.x : 0u - nd.x) : 0u;
-                m_hi += changed ? (y ? nd.y : 0u - nd.y) : 0u;
+                // packed mismatch counters: node i went to y, d = its delta, + d for 0 -> 1, - d for 1 -> 0
+                const uint32_t sg = y - 1u;  // 0 (y = 1) or all ones (y = 0)
+                m_lo += ((fl ? nd.x : 0u) ^ sg) - sg;
+                m_hi += ((fl ? nd.y : 0u) ^ sg) - sg;
                 // bitwise, not short-circuit: no exec-mask branch around the test
                 const bool hz = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
                 const bool hit = act & (((used == 1) & !a.first_tested) ? hit0 : hz);
+                hitf |= hit;
                 act = act & !hit;
             }
             if (__ballot(act) == 0) break;
             }
+            capped = !hitf && used >= a.update_cap;
             done = !act;
         } else
         for (uint32_t c = 0; c < ENV_CHUNK; ++c) {
@@ -1248,8 +1272,8 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast, a.grp)
                                               : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast, a.grp);
     EnvArgs c = a;
-    return launch(fn, grid, env_lds_bytes(W, a.L.bytes, replay ? std::min(a.fast, 1) : a.fast, a.grp), stream, &c,
-                  sizeof c);
+    return launch(fn, grid, env_lds_bytes(W, a.L.bytes + a.erec_shift, replay ? std::min(a.fast, 1) : a.fast, a.grp),
+                  stream, &c, sizeof c);
 }
 
 static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {

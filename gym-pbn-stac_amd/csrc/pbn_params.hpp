@@ -105,6 +105,8 @@ struct EnvArgs {
     int32_t grp;              // fast == 3: lanes per env (2, 4 or 8), k_env_grp
     uint32_t n_calls;         // env steps per env in this launch: actions [n_calls][B][A], outputs
                               // [n_calls][B]...; step t draws with Philox c1 = call_idx + t
+    uint32_t erec_shift;      // fast == 2: LDS bytes the 16-B env records add over the 8-B records
+                              // (off_cubes / off_target / off_ndelta / off_gen are LDS offsets)
 };
 
 constexpr uint32_t MT_ROW = 624;
