@@ -155,10 +155,11 @@ def window_changed_fraction(net, B, device, seed, env_base, warmup, steps):
 
     from gym_pbn_amd.batch import PBNBatch
 
+    dev = torch.device("cuda", device)
     b = PBNBatch(net, B, device=device, seed=seed, env_id_base=env_base)
+    b.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # one stream: the copies and compares in order
     b.randomize()
     b.step(warmup)
-    dev = torch.device("cuda", device)
     x = torch.empty((B, net.n_words), dtype=torch.int64, device=dev)
     y = torch.empty_like(x)
     n = torch.zeros((), dtype=torch.int64, device=dev)
@@ -166,8 +167,9 @@ def window_changed_fraction(net, B, device, seed, env_base, warmup, steps):
         b.get_state_device(x.data_ptr())
         b.step(1)
         b.get_state_device(y.data_ptr())
-        b.sync()
         n += (x != y).any(dim=1).sum()
+    torch.cuda.synchronize(dev)
+    b.set_stream(None)
     b.close()
     return float(n.item()) / (B * steps)
 

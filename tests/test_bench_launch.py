@@ -8,6 +8,8 @@ import subprocess
 import sys
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -32,3 +34,30 @@ def test_gpus_mismatch_with_world_size_fails():
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--check-launch"],
                        capture_output=True, text=True, timeout=120, env=_env(WORLD_SIZE="1", RANK="0"))
     assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.gpu
+def test_window_changed_fraction_matches_host_count():
+    """The roofline's write-back fraction: the twin-batch measurement (device compares on one stream)
+    equals counting changed envs from host copies of the same trajectory, launch by launch."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
+    import bench
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.network import load_network
+
+    net = load_network("bittner199")
+    B, seed, base, W, K = 5000, 0x5EED, 77, 5, 20
+    q = bench.window_changed_fraction(net, B, 0, seed, base, W, K)
+    b = PBNBatch(net, B, seed=seed, env_id_base=base)
+    b.randomize()
+    b.step(W)
+    n = 0
+    for _ in range(K):
+        a = b.get_state()
+        b.step(1)
+        n += int(np.any(a != b.get_state(), axis=1).sum())
+    b.close()
+    assert q == n / (B * K) and 0.2 < q < 0.6
