@@ -107,6 +107,23 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
     b.close()
 
 
+@pytest.mark.parametrize("k", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("name,B", [("bittner199", 70001), ("bittner28", 300001), ("tt200", 40000)])
+def test_envs_per_thread_match_oracle(G, oracle_mod, monkeypatch, k, name, B):
+    """Step mode with 1, 2, 4 or 8 envs per thread (the grid-stride pairs of k_step_single): ragged
+    batches, every env against the oracle, graph-replayed and plain launches."""
+    monkeypatch.setenv("PBNSIM_ENVS_PER_THREAD", k)
+    net = load_network(name)
+    o = oracle_mod.Oracle(net)
+    b = G.PBNBatch(net, B, seed=404, env_id_base=9)
+    b.randomize()
+    init = b.get_state()
+    b.step(3)
+    b.step(1)
+    assert np.array_equal(b.get_state(), o.step_philox(init, 404, 9, 0, 4))
+    b.close()
+
+
 def test_exact_length_step_graphs_match_oracle(G, oracle_mod):
     """pbn_step_prepare(n) captures one graph of exactly n launches without running anything; a
     length called twice in a row gets one too; the batch keeps four lengths (least recently used
