@@ -797,8 +797,8 @@ static bool step_graph_ready(pbn_batch* b) {
     return true;
 }
 
-// Captures n step launches + k_bump(n) as one graph in a free (or the least recently used)
-// exact-length slot. Returns the slot, or -1 (plain launches / power-of-two graphs then).
+// Captures n step launches as one graph in a free (or the least recently used) exact-length slot.
+// Returns the slot, or -1 (plain launches / power-of-two graphs then).
 static int exact_graph_build(pbn_batch* b, uint32_t n) {
     if (n < 2 || n > STEP_GRAPH_K || b->step_graph_broken || b->step_graph_off || !b->stream) return -1;
     if (b->s_ubase.ensure(64)) return -1;
