@@ -151,6 +151,7 @@ struct pbn_batch {
     uint32_t env_calls = 0, reset_count = 0;
     int env_lanes = 0;  // lanes per env of the last R6 launch
     int env_grid_last = 0;  // workgroups of the last R6 launch
+    int env_kernel_last = -1;  // pbn_batch_info.env_kernel of the last R6 launch
     uint64_t* d_state = nullptr;
     int64_t* d_nsteps = nullptr;
     int32_t* d_error = nullptr;
@@ -554,6 +555,7 @@ int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
     info->env_lanes = b->env_lanes;
     info->roll_lanes = b->roll_group;
     info->env_grid = b->env_grid_last;
+    info->env_kernel = b->env_kernel_last;
     return 0;
 }
 
@@ -1286,6 +1288,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         if (nrec > 65535u || env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1) > 64u * 1024u) {
             mode = cfg->fast;  // too large for the u16 record index / one workgroup's LDS
             erec_shift = 0;
+        } else if (cfg->H <= 4) {
+            mode = 4;  // the same kernel with one packed counter word (<= 4 cubes)
         }
     }
     int bpc = 1;
@@ -1341,6 +1345,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     if (!replay) b->env_calls += n_calls;
     b->env_lanes = grp;
     b->env_grid_last = grid;
+    b->env_kernel_last = replay ? std::min(mode, 1) : mode;
     return 0;
 }
 

@@ -350,7 +350,8 @@ __device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* c
 // negation), and "some cube matches" is a zero-byte test -- a handful of VALU ops
 // per update. Otherwise the state is matched against every cube after a change.
 //
-// GEN (FAST == 2, predictor-mix networks, Philox): before each chunk the whole wave
+// GEN (FAST == 2, or 4 with <= 4 cubes: one counter word; predictor-mix networks, Philox):
+// before each chunk the whole wave
 // generates the chunk's draws for all its active lanes -- assignment k of
 // n_active * ENV_CHUNK goes to lane k % 64 -- and stores (node, chosen predictor) as
 // u16 in a per-wave LDS buffer; the lanes then only apply the records. With every lane
@@ -364,10 +365,12 @@ constexpr uint32_t ENV_OWN_DRAWS_MIN = 40;  // active lanes from which a wave sk
 
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
-    static_assert(FAST != 2 || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
+    constexpr bool GEN = FAST == 2 || FAST == 4;
+    constexpr bool ONE_WORD = FAST == 4;  // <= 4 cubes: the high counter word is never read
+    static_assert(!GEN || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
     extern __shared__ __align__(16) uint8_t lds[];
     const uint32_t N = (uint32_t)a.L.n_nodes;
-    if constexpr (FAST == 2) {
+    if constexpr (GEN) {
         // LDS: the thresholds as staged; in place of the 8-B predictor records, 16-B "env
         // records" (EnvRec) carrying each input's plane offset and bit position, so an update
         // does no index arithmetic; the cubes / target / deltas after them move up by erec_shift
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             continue;
         }
         uint16_t* gbuf = nullptr;
-        if constexpr (FAST == 2) {
+        if constexpr (GEN) {
             // ---- cooperative draw generation for the next ENV_CHUNK updates of every active lane
             uint8_t* gw = lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES;
             gbuf = reinterpret_cast<uint16_t*>(gw);                                   // [ENV_CHUNK][64]
@@ -534,7 +537,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         // ---- up to ENV_CHUNK updates of this lane's env
         const uint64_t g = a.env_base + (uint64_t)e;
         bool done = false;
-        if constexpr (FAST == 2) {
+        if constexpr (GEN) {
             const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
             const uint8_t* pb = reinterpret_cast<const uint8_t*>(P.base);  // this lane's plane column
             // branch-free per lane: a lane that is done keeps iterating masked (no break, so
@@ -549,11 +552,39 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             uint2 n0 = ndelta[q0.w >> 16];
             uint32_t e2 = gbuf[128 + lane];
             static_assert(ENV_CHUNK >= 3 && ENV_CHUNK % ENV_UNROLL == 0, "prefetch depth / unroll");
+            // Update c's counter update and attractor test are made after update c + 1's plane
+            // reads are issued, while they are in flight: they only decide whether c + 1 is
+            // applied (its act), so the dependent chain from one plane write to the next is the
+            // LDS round trip and the y / write work, not also the counters (in source order the
+            // wave issues them in between). pfl / psg / pnd carry update c's outcome.
+            uint32_t pfl = 0u, psg = 0u;
+            uint2 pnd = make_uint2(0u, 0u);
+            // packed mismatch counters: node i went to y, d = its delta, + d for 0 -> 1, - d for 1 -> 0;
+            // then the test after that update (bitwise, no exec-mask branch around it)
+            // (the select between the first-update test and the counters' test is written as
+            // bit arithmetic: as a ?: the compiler branched around the counters' test)
+            // :134 the first update of an env step is tested on o0: "first" is 1 when the update
+            // being settled is it (used == 1 after it; in the chunk, update 1's settle with used 0
+            // at the chunk's start)
+            const uint32_t h0 = hit0 ? 1u : 0u;
+            const uint32_t f1 = (used == 0u && !a.first_tested) ? 1u : 0u;
+            auto settle = [&](uint32_t pending, uint32_t first) {
+                m_lo += ((pfl ? pnd.x : 0u) ^ psg) - psg;
+                uint32_t zb = has_zero_byte(m_lo);
+                if constexpr (!ONE_WORD) {
+                    m_hi += ((pfl ? pnd.y : 0u) ^ psg) - psg;
+                    zb |= has_zero_byte(m_hi);
+                }
+                const uint32_t z = zb != 0u ? 1u : 0u;
+                const bool hit = act & (((z ^ (first & (z ^ h0))) & pending) != 0u);
+                hitf |= hit;
+                act = act & !hit;
+            };
             // the wave tests for "no lane active" once per ENV_UNROLL updates, not per update: the
             // per-update ballot + branch made every update wait for the whole previous one (the
-            // wave cannot issue past an unresolved branch), so the state chain of update c + 1
-            // could not overlap the counters / attractor test of update c. Lanes that finish
-            // inside a block run its remaining updates masked (act = 0: nothing is written).
+            // wave cannot issue past an unresolved branch). Lanes that finish inside a block run
+            // its remaining updates masked (act = 0: nothing is written); the test sees act before
+            // the block's last update is settled, so a wave may run one masked block more.
             for (uint32_t c0 = 0; c0 < ENV_CHUNK; c0 += ENV_UNROLL) {
 #pragma unroll
             for (uint32_t u = 0; u < ENV_UNROLL; ++u) {
@@ -565,12 +596,13 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 q0 = q1;
                 q1 = erec[e2];
                 e2 = gbuf[min(c + 3, ENV_CHUNK - 1) * 64 + lane];
-                act = act & (c < lim);  // the update cap (pbn_target_multi.py's loop is unbounded)
                 // Predstep (base.py:100-118): Y = tt[x_in0 x_in1 x_in2 x_self] from the plane
                 const uint32_t b0 = *reinterpret_cast<const uint32_t*>(pb + (q.x & 0xFFFFu));
                 const uint32_t b1 = *reinterpret_cast<const uint32_t*>(pb + (q.x >> 16));
                 const uint32_t b2 = *reinterpret_cast<const uint32_t*>(pb + (q.y & 0xFFFFu));
                 const uint32_t self = *reinterpret_cast<const uint32_t*>(pb + (q.y >> 16));
+                settle(c != 0 ? 1u : 0u, c == 1 ? f1 : 0u);  // update c - 1 (nothing pending before the chunk's first)
+                act = act & (c < lim);  // the update cap (pbn_target_multi.py's loop is unbounded)
                 const uint32_t shs = q.z >> 24;
                 const uint32_t xs = __builtin_amdgcn_ubfe(self, shs, 1);
                 const uint32_t p = (__builtin_amdgcn_ubfe(b0, q.z, 1) << 3) |
@@ -580,18 +612,13 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 const uint32_t fl = (xs ^ y) & (act ? 1u : 0u);  // the bit changes (and is applied)
                 *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(pb) + (q.y >> 16)) = self ^ (fl << shs);
                 used += act ? 1u : 0u;
-                // packed mismatch counters: node i went to y, d = its delta, + d for 0 -> 1, - d for 1 -> 0
-                const uint32_t sg = y - 1u;  // 0 (y = 1) or all ones (y = 0)
-                m_lo += ((fl ? nd.x : 0u) ^ sg) - sg;
-                m_hi += ((fl ? nd.y : 0u) ^ sg) - sg;
-                // bitwise, not short-circuit: no exec-mask branch around the test
-                const bool hz = (has_zero_byte(m_lo) | has_zero_byte(m_hi)) != 0u;
-                const bool hit = act & (((used == 1) & !a.first_tested) ? hit0 : hz);
-                hitf |= hit;
-                act = act & !hit;
+                pfl = fl;
+                psg = y - 1u;  // 0 (y = 1) or all ones (y = 0)
+                pnd = nd;
             }
             if (__ballot(act) == 0) break;
             }
+            settle(1u, (used == 1u && !a.first_tested) ? 1u : 0u);  // the last update made
             capped = !hitf && used >= a.update_cap;
             done = !act;
         } else
@@ -1143,6 +1170,7 @@ static void* env_fn_w(int W, int replay, int fast, int grp) {
 #define PBN_ENV_CASE(w)                                                                  \
     case w:                                                                              \
         if (fast == 2 && KIND == KIND_PREDICTOR_MIX && !replay) return (void*)k_env<w, KIND_PREDICTOR_MIX, 0, 2>; \
+        if (fast == 4 && KIND == KIND_PREDICTOR_MIX && !replay) return (void*)k_env<w, KIND_PREDICTOR_MIX, 0, 4>; \
         if (fast) return replay ? (void*)k_env<w, KIND, 1, 1> : (void*)k_env<w, KIND, 0, 1>; \
         return replay ? (void*)k_env<w, KIND, 1, 0> : (void*)k_env<w, KIND, 0, 0>;
     switch (W) {
@@ -1298,7 +1326,7 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp) {
     if (fast == 3) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
     const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
-    return fast == 2 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES : planes;
+    return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES : planes;
 }
 
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu) {

@@ -92,8 +92,9 @@ struct EnvArgs {
     int32_t n_cubes;
     int32_t fast;            // 1: <= 8 cubes, each caring about <= 255 nodes (byte counters);
                              // 2: and predictor mix with <= 16 predictors per node, Philox: the
-                             //    draws are generated cooperatively by the whole wave
-    uint32_t off_gen;        // fast == 2: per-wave draw buffers (ENV_GEN_WAVE_BYTES each);
+                             //    draws are generated cooperatively by the whole wave;
+                             // 3: group mode (k_env_grp); 4: as 2 with <= 4 cubes (one counter word)
+    uint32_t off_gen;        // fast == 2 / 4: per-wave draw buffers (ENV_GEN_WAVE_BYTES each);
                              // fast == 3: per-group env rows (2W dwords per group of grp lanes)
     uint64_t B, env_base, seed;
     uint32_t call_idx, update_cap;

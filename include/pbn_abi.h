@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 10
+#define PBN_ABI_VERSION 11
 
 enum {
     PBN_OK = 0,
@@ -84,6 +84,8 @@ typedef struct {
     int32_t env_lanes; /* last R6 env-step launch: 1 = one lane per env (k_env), 2/4/8 = lanes per env (k_env_grp) */
     int32_t roll_lanes; /* rollout kernel: 1 = one lane per env (k_rollout), 2/4/8 = lanes per env (k_rollout_grp) */
     int32_t env_grid;   /* last R6 env-step launch: workgroups (256 lanes each; lanes refill from a work counter) */
+    int32_t env_kernel; /* last R6 env-step launch: 0 = cube matching, 1 = byte counters, 2 = byte counters +
+                           wave-generated draws, 3 = group mode (k_env_grp), 4 = 2 with one counter word (<= 4 cubes) */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).

@@ -594,7 +594,8 @@ def _random_cubes(rng, N, H, n_care):
     return cubes
 
 
-@pytest.mark.parametrize("case", ["b28_gen_cap", "b28_h12_general", "b199_nogen", "tt200_fast", "syn500_gen",
+@pytest.mark.parametrize("case", ["b28_gen_cap", "b28_h8_gen", "b199_h6_gen_first_tested", "b28_h12_general",
+                                  "b199_nogen", "tt200_fast", "syn500_gen",
                                   "syn300_wide_cube", "b28_first_tested", "b28_h12_first_tested",
                                   "tt200_first_tested", "b199_grp2", "b199_grp4", "b199_grp8", "b28_grp4_cap",
                                   "b28_grp8_first_tested", "b28_grp2_h8", "b199_grp4_long"])
@@ -612,6 +613,8 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
         net = load_network("bittner199")
     elif case.startswith("b28"):
         net = load_network("bittner28")
+    elif case == "b199_h6_gen_first_tested":
+        net = load_network("bittner199")
     elif case == "b199_nogen":
         net = load_network("bittner199")
         monkeypatch.setenv("PBNSIM_ENV_NO_GEN", "1")
@@ -627,8 +630,10 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     elif case == "b199_grp4_long":  # long until-attractor loops, many capped envs
         cap = 2001
         attractors = [_random_cubes(rng, N, 4, 12), _random_cubes(rng, N, 2, 4)]
-    elif case == "b28_grp2_h8":  # 8 cubes: the most the byte counters hold
+    elif case in ("b28_grp2_h8", "b28_h8_gen"):  # 8 cubes: the most the byte counters hold
         attractors = [_random_cubes(rng, N, 4, 4), _random_cubes(rng, N, 4, 4)]
+    elif case == "b199_h6_gen_first_tested":  # 5..8 cubes: both packed counter words
+        attractors = [_random_cubes(rng, N, 3, 3), _random_cubes(rng, N, 3, 3)]
     elif case.startswith("b28_h12"):
         attractors = [_random_cubes(rng, N, 6, 4), _random_cubes(rng, N, 6, 4)]
     elif case == "syn300_wide_cube":  # one cube caring about 260 > 255 nodes: general matching
@@ -656,6 +661,10 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
         assert np.array_equal(b.get_state(), st), case
         if "_grp" in case:
             assert b.info()["env_lanes"] == int(case.split("_grp")[1][0])  # group mode really ran
+        if case in ("b28_gen_cap", "b28_first_tested"):
+            assert b.info()["env_kernel"] == 4  # wave-generated draws, one counter word (<= 4 cubes)
+        if case in ("b28_h8_gen", "b199_h6_gen_first_tested"):
+            assert b.info()["env_kernel"] == 2  # wave-generated draws, two counter words
     if case in ("b28_gen_cap", "b28_grp4_cap", "b199_grp4_long"):
         assert (flags & 4).any() and not (flags & 4).all()  # some envs capped, some reached an attractor
     assert (nup > 1).any()
