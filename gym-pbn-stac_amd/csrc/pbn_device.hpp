@@ -49,6 +49,12 @@ __device__ __forceinline__ void philox_draw(uint64_t seed, uint32_t c0, uint32_t
     philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// R6 env stream (STREAM_ENV, k_env / k_env_grp): update u of an env step takes Philox call u >> 1,
+// so one call serves two updates -- node from word 2(u & 1), the predictor-choice uniform from
+// word 2(u & 1) + 1 as k53 = a << 21 | a >> 11: 32 random bits spread over the 53-bit grid
+// (monotone in a; choice probabilities exact to 2^-32). Shared with oracle/pbn_oracle.c env_k53.
+__device__ __forceinline__ uint64_t env_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
+
 // random() == k53 * 2^-53, built CPython-style from two words (a>>5, b>>6).
 __device__ __forceinline__ uint64_t k53_of(uint32_t a, uint32_t b) {
     return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);

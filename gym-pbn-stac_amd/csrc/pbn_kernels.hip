@@ -493,13 +493,17 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 // -- no rank / counter tables; an idle lane's draws are junk nobody reads. Fewer
                 // rounds shared over the wave stop paying off below ~40 active lanes (a shared
                 // round costs two dependent LDS round trips more)
+                // (a chunk starts at an even update index: one Philox call per pair of updates)
                 const uint64_t gid = a.env_base + (uint64_t)e;
-                for (uint32_t sl = 0; sl < ENV_CHUNK; ++sl) {
+                for (uint32_t sl = 0; sl < ENV_CHUNK; sl += 2) {
                     uint32_t w[4];
-                    philox_draw(a.seed, used + sl, a.call_idx + t, gid, STREAM_ENV, w);
-                    const uint32_t i = philox_node<KIND>(w[0], N);
-                    const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
-                    gbuf[sl * 64 + lane] = (uint16_t)(__umul24(i, a.L.pmax) + j);  // EnvRec index
+                    philox_draw(a.seed, (used + sl) >> 1, a.call_idx + t, gid, STREAM_ENV, w);
+#pragma unroll
+                    for (uint32_t h = 0; h < 2; ++h) {
+                        const uint32_t i = philox_node<KIND>(w[2 * h], N);
+                        const uint32_t j = predictor_choice(i, env_k53(w[2 * h + 1]), lds, a.L);
+                        gbuf[(sl + h) * 64 + lane] = (uint16_t)(__umul24(i, a.L.pmax) + j);  // EnvRec index
+                    }
                 }
             } else {
             if (e >= 0) {
@@ -511,20 +515,23 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t total = nact * ENV_CHUNK;
+            const uint32_t total = nact * (ENV_CHUNK / 2);  // pairs of updates: one Philox call each
             // k / nact as a multiply-high by ceil(2^32 / nact): exact for k < 2^16 (nact == 1 handled apart,
             // its multiplier 2^32 does not fit 32 bits)
             const uint32_t magic = nact > 1 ? (uint32_t)((0x100000000ull + nact - 1) / nact) : 0u;
             for (uint32_t k0 = 0; k0 < total; k0 += 64) {
                 const uint32_t k = k0 + lane;
                 if (k < total) {
-                    const uint32_t sl = nact > 1 ? __umulhi(k, magic) : k, r = k - sl * nact;
+                    const uint32_t sp = nact > 1 ? __umulhi(k, magic) : k, r = k - sp * nact;
                     const uint32_t q = lane_of_rank[r];
                     uint32_t w[4];
-                    philox_draw(a.seed, used_tab[q] + sl, call_tab[q], gid_tab[q], STREAM_ENV, w);
-                    const uint32_t i = philox_node<KIND>(w[0], N);
-                    const uint32_t j = predictor_choice(i, k53_of(w[1], w[2]), lds, a.L);
-                    gbuf[sl * 64 + q] = (uint16_t)(__umul24(i, a.L.pmax) + j);
+                    philox_draw(a.seed, (used_tab[q] >> 1) + sp, call_tab[q], gid_tab[q], STREAM_ENV, w);
+#pragma unroll
+                    for (uint32_t h = 0; h < 2; ++h) {
+                        const uint32_t i = philox_node<KIND>(w[2 * h], N);
+                        const uint32_t j = predictor_choice(i, env_k53(w[2 * h + 1]), lds, a.L);
+                        gbuf[(2 * sp + h) * 64 + q] = (uint16_t)(__umul24(i, a.L.pmax) + j);
+                    }
                 }
             }
             }
@@ -641,9 +648,10 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 ++dpos;
             } else {
                 uint32_t w[4];
-                philox_draw(a.seed, used, a.call_idx + t, g, STREAM_ENV, w);
-                i = philox_node<KIND>(w[0], N);
-                k53 = k53_of(w[1], w[2]);
+                philox_draw(a.seed, used >> 1, a.call_idx + t, g, STREAM_ENV, w);
+                const bool odd = (used & 1u) != 0u;
+                i = philox_node<KIND>(odd ? w[2] : w[0], N);
+                k53 = env_k53(odd ? w[3] : w[1]);
             }
             uint32_t changed;
             if constexpr (KIND == KIND_PREDICTOR_MIX)
@@ -947,10 +955,11 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
         }
 
         // ---- one block: update used + k of this group's env in lane k (idle groups compute junk)
+        // (a block starts at a multiple of G: lanes 2m and 2m + 1 share Philox call (used >> 1) + m)
         uint32_t w4[4];
-        philox_draw(a.seed, used + k, a.call_idx + t, gid, STREAM_ENV, w4);
-        const uint32_t i = philox_node<KIND_PREDICTOR_MIX>(w4[0], N);
-        const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, k53_of(w4[1], w4[2]), lds, a.L)];
+        philox_draw(a.seed, (used + k) >> 1, a.call_idx + t, gid, STREAM_ENV, w4);
+        const uint32_t i = philox_node<KIND_PREDICTOR_MIX>((k & 1u) ? w4[2] : w4[0], N);
+        const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, env_k53((k & 1u) ? w4[3] : w4[1]), lds, a.L)];
         const uint2 nd = ndelta[i];
         const uint32_t in[4] = {(uint32_t)rec & 0xFFFFu, (uint32_t)(rec >> 16) & 0xFFFFu,
                                 (uint32_t)(rec >> 32) & 0xFFFFu, i};

@@ -223,6 +223,9 @@ static inline int philox_node(const orc_net *n, uint32_t w0) {
 }
 
 static inline uint64_t philox_k53(const uint32_t w[4]) { return ((uint64_t)(w[1] >> 5) << 26) | (w[2] >> 6); }
+/* R6 env stream (STREAM_ENV): update u takes Philox call u >> 1, node from word 2(u & 1), the
+ * predictor-choice uniform from word 2(u & 1) + 1 as k53 = a << 21 | a >> 11 (pbn_device.hpp env_k53) */
+static inline uint64_t env_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
 
 /* --------------------------------------------------------------- step modes */
 /* Replay: node_idx/k53 are [T][B] (the draws the reference made). */
@@ -416,9 +419,10 @@ EXPORT int orc_env_step_multi(const orc_net *n, const orc_envcfg *c, uint64_t *s
                 dpos++;
             } else {
                 uint32_t w[4];
-                philox_draw(seed, used, call_idx, env_base + (uint64_t)e, STREAM_ENV, w);
-                i = philox_node(n, w[0]);
-                k53 = philox_k53(w);
+                philox_draw(seed, used >> 1, call_idx, env_base + (uint64_t)e, STREAM_ENV, w);
+                const int h = (int)(used & 1u);
+                i = philox_node(n, w[2 * h]);
+                k53 = env_k53(w[2 * h + 1]);
             }
             node_update(n, s, i, k53);
             used++;
