@@ -55,6 +55,14 @@ __device__ __forceinline__ void philox_draw(uint64_t seed, uint32_t c0, uint32_t
 // (monotone in a; choice probabilities exact to 2^-32). Shared with oracle/pbn_oracle.c env_k53.
 __device__ __forceinline__ uint64_t env_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
 
+// Threshold T re-expressed on a: the smallest a with env_k53(a) >= T (2^32 = never), so that
+// env_k53(a) >= T <=> a >= env_threshold(T) (env_k53 is monotone; env_k53(T >> 21 - 1) < T).
+__device__ __forceinline__ uint64_t env_threshold(uint64_t T) {
+    const uint64_t a0 = T >> 21;
+    if (a0 >= (1ull << 32)) return 1ull << 32;
+    return env_k53((uint32_t)a0) >= T ? a0 : a0 + 1u;
+}
+
 // random() == k53 * 2^-53, built CPython-style from two words (a>>5, b>>6).
 __device__ __forceinline__ uint64_t k53_of(uint32_t a, uint32_t b) {
     return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);

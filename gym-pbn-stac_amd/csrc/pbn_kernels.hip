@@ -376,7 +376,12 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         // does no index arithmetic; the cubes / target / deltas after them move up by erec_shift
         const uint4* g = reinterpret_cast<const uint4*>(a.img);
         uint4* l = reinterpret_cast<uint4*>(lds);
-        for (uint32_t k = threadIdx.x; k < a.L.off_rec / 16; k += BLOCK) l[k] = g[k];
+        // the thresholds ([0, off_rec) of a predictor-mix image) re-expressed on the draw word a
+        // (env_threshold), so the choice compares a itself: no k53 to build per draw
+        for (uint32_t k = threadIdx.x; k < a.L.off_rec / 16; k += BLOCK) {
+            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(g)[k];
+            reinterpret_cast<ulonglong2*>(l)[k] = make_ulonglong2(env_threshold(v.x), env_threshold(v.y));
+        }
         const uint32_t tail = a.off_cubes - a.erec_shift;  // the cubes' offset in the device image
         for (uint32_t k = threadIdx.x; k < (a.L.bytes - tail) / 16; k += BLOCK)
             l[(tail + a.erec_shift) / 16 + k] = g[tail / 16 + k];
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
                     for (uint32_t h = 0; h < 2; ++h) {
                         const uint32_t i = philox_node<KIND>(w[2 * h], N);
-                        const uint32_t j = predictor_choice(i, env_k53(w[2 * h + 1]), lds, a.L);
+                        const uint32_t j = predictor_choice(i, (uint64_t)w[2 * h + 1], lds, a.L);
                         gbuf[(sl + h) * 64 + lane] = (uint16_t)(__umul24(i, a.L.pmax) + j);  // EnvRec index
                     }
                 }
@@ -529,7 +534,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
                     for (uint32_t h = 0; h < 2; ++h) {
                         const uint32_t i = philox_node<KIND>(w[2 * h], N);
-                        const uint32_t j = predictor_choice(i, env_k53(w[2 * h + 1]), lds, a.L);
+                        const uint32_t j = predictor_choice(i, (uint64_t)w[2 * h + 1], lds, a.L);
                         gbuf[(2 * sp + h) * 64 + q] = (uint16_t)(__umul24(i, a.L.pmax) + j);
                     }
                 }
@@ -592,6 +597,9 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             // wave cannot issue past an unresolved branch). Lanes that finish inside a block run
             // its remaining updates masked (act = 0: nothing is written); the test sees act before
             // the block's last update is settled, so a wave may run one masked block more.
+            // The cap test is compiled in only for chunks where some lane of the wave can reach
+            // the cap (lim < ENV_CHUNK); the other chunks run the loop without it.
+            auto chunk = [&](auto cap_near) {
             for (uint32_t c0 = 0; c0 < ENV_CHUNK; c0 += ENV_UNROLL) {
 #pragma unroll
             for (uint32_t u = 0; u < ENV_UNROLL; ++u) {
@@ -609,7 +617,8 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 const uint32_t b2 = *reinterpret_cast<const uint32_t*>(pb + (q.y & 0xFFFFu));
                 const uint32_t self = *reinterpret_cast<const uint32_t*>(pb + (q.y >> 16));
                 settle(c != 0 ? 1u : 0u, c == 1 ? f1 : 0u);  // update c - 1 (nothing pending before the chunk's first)
-                act = act & (c < lim);  // the update cap (pbn_target_multi.py's loop is unbounded)
+                if constexpr (decltype(cap_near)::value)
+                    act = act & (c < lim);  // the update cap (pbn_target_multi.py's loop is unbounded)
                 const uint32_t shs = q.z >> 24;
                 const uint32_t xs = __builtin_amdgcn_ubfe(self, shs, 1);
                 const uint32_t p = (__builtin_amdgcn_ubfe(b0, q.z, 1) << 3) |
@@ -625,6 +634,11 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             }
             if (__ballot(act) == 0) break;
             }
+            };
+            if (__ballot(lim < ENV_CHUNK) != 0)
+                chunk(std::true_type{});
+            else
+                chunk(std::false_type{});
             settle(1u, (used == 1u && !a.first_tested) ? 1u : 0u);  // the last update made
             capped = !hitf && used >= a.update_cap;
             done = !act;
