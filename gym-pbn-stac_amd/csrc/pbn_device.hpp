@@ -49,18 +49,52 @@ __device__ __forceinline__ void philox_draw(uint64_t seed, uint32_t c0, uint32_t
     philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-// R6 env stream (STREAM_ENV, k_env / k_env_grp): update u of an env step takes Philox call u >> 1,
-// so one call serves two updates -- node from word 2(u & 1), the predictor-choice uniform from
-// word 2(u & 1) + 1 as k53 = a << 21 | a >> 11: 32 random bits spread over the 53-bit grid
-// (monotone in a; choice probabilities exact to 2^-32). Shared with oracle/pbn_oracle.c env_k53.
-__device__ __forceinline__ uint64_t env_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
+// Draws of the step and R6 streams use two 32-bit words per update: the node word and the
+// predictor-choice uniform a, taken as k53 = a << 21 | a >> 11 (32 random bits spread over the
+// 53-bit grid, monotone in a, so the integer thresholds decide the choice exactly; choice
+// probabilities exact to 2^-32). One Philox call (four words) thus serves two updates:
+//   STREAM_STEP: update u of env g takes call {u, g >> 1}, words 2(g & 1) and 2(g & 1) + 1 (envs
+//                2m and 2m + 1 share a call);
+//   STREAM_ENV:  update u of an env step takes call {u >> 1, call index}, words 2(u & 1), +1.
+// Shared with oracle/pbn_oracle.c (u32_k53, step_words).
+__device__ __forceinline__ uint64_t u32_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
 
-// Threshold T re-expressed on a: the smallest a with env_k53(a) >= T (2^32 = never), so that
-// env_k53(a) >= T <=> a >= env_threshold(T) (env_k53 is monotone; env_k53(T >> 21 - 1) < T).
-__device__ __forceinline__ uint64_t env_threshold(uint64_t T) {
+// Threshold T re-expressed on a: the smallest a with u32_k53(a) >= T (2^32 = never), so that
+// u32_k53(a) >= T <=> a >= u32_threshold(T) (u32_k53 is monotone; u32_k53(T >> 21 - 1) < T).
+__device__ __forceinline__ uint64_t u32_threshold(uint64_t T) {
     const uint64_t a0 = T >> 21;
     if (a0 >= (1ull << 32)) return 1ull << 32;
-    return env_k53((uint32_t)a0) >= T ? a0 : a0 + 1u;
+    return u32_k53((uint32_t)a0) >= T ? a0 : a0 + 1u;
+}
+
+// Lanes 2k and 2k + 1 swap a word (DPP quad_perm [1,0,3,2]). A lane whose partner is inactive
+// gets its own value back.
+__device__ __forceinline__ uint32_t swap_pair_lanes(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false);
+}
+
+// STREAM_STEP words of update u for this lane's env g and env g + 2j (same parity), when lanes
+// 2k / 2k + 1 hold envs 2m / 2m + 1 (even env base): each lane computes ONE call -- the even lane
+// the call of its first env's pair, the odd lane that of its second env's pair -- and the pair
+// swaps the two words the other needs. n*/c* = node word / choice word of the two envs.
+__device__ __forceinline__ void step_words_paired(uint64_t seed, uint64_t u, uint64_t g0, uint64_t g1, bool odd,
+                                                  uint32_t& n0, uint32_t& c0, uint32_t& n1, uint32_t& c1) {
+    uint32_t w[4];
+    philox_draw(seed, (uint32_t)u, (uint32_t)(u >> 32), (odd ? g1 : g0) >> 1, STREAM_STEP, w);
+    const uint32_t r0 = swap_pair_lanes(odd ? w[0] : w[2]), r1 = swap_pair_lanes(odd ? w[1] : w[3]);
+    n0 = odd ? r0 : w[0];
+    c0 = odd ? r1 : w[1];
+    n1 = odd ? w[2] : r0;
+    c1 = odd ? w[3] : r1;
+}
+
+// STREAM_STEP words of update u for env g alone (one call per env).
+__device__ __forceinline__ void step_words(uint64_t seed, uint64_t u, uint64_t g, uint32_t& n, uint32_t& c) {
+    uint32_t w[4];
+    philox_draw(seed, (uint32_t)u, (uint32_t)(u >> 32), g >> 1, STREAM_STEP, w);
+    const bool h = (g & 1u) != 0u;
+    n = h ? w[2] : w[0];
+    c = h ? w[3] : w[1];
 }
 
 // random() == k53 * 2^-53, built CPython-style from two words (a>>5, b>>6).

@@ -50,14 +50,25 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
     uint64_t nxt[W];
     uint32_t i0 = 0, i1 = 0;
     uint64_t q0 = 0, q1 = 0;
+    // envs 2m / 2m + 1 share a Philox call (pbn_device.hpp): with an even env base, lane parity is
+    // env parity and the lane pair computes one call per env pair each (step_words_paired). A
+    // partner lane that has left the loop holds envs >= B only, so the words it no longer sends
+    // belong to envs that are not applied.
+    const bool paired = (a.env_base & 1u) == 0u;
+    const bool odd = (threadIdx.x & 1u) != 0u;
     auto draws = [&](uint64_t ea) {
-        uint32_t w0[4], w1[4];
-        philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), a.env_base + ea, STREAM_STEP, w0);
-        philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), a.env_base + ea + po, STREAM_STEP, w1);
-        i0 = philox_node<KIND>(w0[0], N);
-        i1 = philox_node<KIND>(w1[0], N);
-        q0 = k53_of(w0[1], w0[2]);
-        q1 = k53_of(w1[1], w1[2]);
+        const uint64_t g0 = a.env_base + ea, g1 = g0 + po;
+        uint32_t n0, c0, n1, c1;
+        if (paired) {
+            step_words_paired(a.seed, u, g0, g1, odd, n0, c0, n1, c1);
+        } else {
+            step_words(a.seed, u, g0, n0, c0);
+            step_words(a.seed, u, g1, n1, c1);
+        }
+        i0 = philox_node<KIND>(n0, N);
+        i1 = philox_node<KIND>(n1, N);
+        q0 = u32_k53(c0);
+        q1 = u32_k53(c1);
     };
     if (e + po < a.B) load_state<W>(a.state + (e + po) * W, nxt);
     draws(e);
@@ -172,44 +183,75 @@ __global__ __launch_bounds__(SB) void k_rollout(StepArgs a) {
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
-    while (e < a.B) {
+    // Envs 2m / 2m + 1 share their Philox calls (pbn_device.hpp). With an even env base the lane
+    // pair holds such a pair, and for updates t, t + 1 the even lane computes the call of t, the
+    // odd lane that of t + 1, and they swap the two words the other needs: one call per lane
+    // per two updates. Every lane of a wave takes the same trips (lanes past B compute junk
+    // and store nothing), so a partner is never missing.
+    const bool paired = (a.env_base & 1u) == 0u;
+    const bool odd = (threadIdx.x & 1u) != 0u;
+    for (;;) {
+        const bool live = e < a.B;
+        if (__ballot(live) == 0) break;
         const uint64_t en = e + stride;
         uint64_t nxt[W];
         if (en < a.B) load_state<W>(a.state + en * W, nxt);  // prefetch the next env
         to_plane<W>(P, cur);
         uint32_t changed = 0;
         const uint64_t g = a.env_base + e;
-        if constexpr (KIND == KIND_PREDICTOR_MIX) {
-            // software pipeline: the draw and predictor record of update t + 1 (state-independent)
-            // are computed while update t's plane read is in flight -- one env per lane leaves a
-            // wave alone on its SIMD at small batches (65,536 envs: one wave per SIMD)
-            auto draw = [&](uint32_t t, uint32_t* i, uint64_t* rec) {
-                const uint64_t u = a.update_base + t;
+        // node / choice words of updates t and t + 1 of this lane's env
+        auto words2 = [&](uint32_t t, uint32_t& na, uint32_t& ca, uint32_t& nb, uint32_t& cb) {
+            const uint64_t u = a.update_base + t;
+            if (paired) {
                 uint32_t w[4];
-                philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
-                *i = philox_node<KIND>(w[0], N);
-                *rec = predictor_record(*i, k53_of(w[1], w[2]), lds, a.L);
+                philox_draw(a.seed, (uint32_t)(u + (odd ? 1u : 0u)), (uint32_t)((u + (odd ? 1u : 0u)) >> 32), g >> 1,
+                            STREAM_STEP, w);
+                const uint32_t r0 = swap_pair_lanes(odd ? w[0] : w[2]), r1 = swap_pair_lanes(odd ? w[1] : w[3]);
+                na = odd ? r0 : w[0];
+                ca = odd ? r1 : w[1];
+                nb = odd ? w[2] : r0;
+                cb = odd ? w[3] : r1;
+            } else {
+                step_words(a.seed, u, g, na, ca);
+                step_words(a.seed, u + 1u, g, nb, cb);
+            }
+        };
+        if constexpr (KIND == KIND_PREDICTOR_MIX) {
+            // software pipeline: the draws and predictor records of updates t + 2, t + 3
+            // (state-independent) are computed while updates t, t + 1 run -- one env per lane
+            // leaves a wave alone on its SIMD at small batches (65,536 envs: one wave per SIMD)
+            uint32_t ia, ib;
+            uint64_t ra, rb;
+            auto draw2 = [&](uint32_t t) {
+                uint32_t na, ca, nb, cb;
+                words2(t, na, ca, nb, cb);
+                ia = philox_node<KIND>(na, N);
+                ib = philox_node<KIND>(nb, N);
+                ra = predictor_record(ia, u32_k53(ca), lds, a.L);
+                rb = predictor_record(ib, u32_k53(cb), lds, a.L);
             };
-            uint32_t i1;
-            uint64_t r1;
-            draw(0, &i1, &r1);
-            for (uint32_t t = 0; t < a.T; ++t) {
-                const uint32_t i = i1;
-                const uint64_t rec = r1;
-                draw(min(t + 1, a.T - 1), &i1, &r1);  // unconditional: no branch before the plane read
+            auto apply = [&](uint32_t i, uint64_t rec) {
                 const uint32_t d = i >> 5, sh = i & 31u;
                 const uint32_t self = P.get(d);
                 const uint32_t y = predictor_apply(P, i, self, rec);
                 const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
                 P.put(d, nv);
                 changed |= nv != self;
+            };
+            draw2(0);
+            for (uint32_t t = 0; t < a.T; t += 2) {
+                const uint32_t i0 = ia, i1 = ib;
+                const uint64_t r0 = ra, r1 = rb;
+                draw2(t + 2);  // unconditional (past T: junk, unused): no branch before the plane reads
+                apply(i0, r0);
+                if (t + 1 < a.T) apply(i1, r1);
             }
         } else {
-            for (uint32_t t = 0; t < a.T; ++t) {
-                const uint64_t u = a.update_base + t;
-                uint32_t w[4];
-                philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
-                changed |= table_update_lds(P, philox_node<KIND>(w[0], N), k53_of(w[1], w[2]), lds, a.L);
+            for (uint32_t t = 0; t < a.T; t += 2) {
+                uint32_t na, ca, nb, cb;
+                words2(t, na, ca, nb, cb);
+                changed |= table_update_lds(P, philox_node<KIND>(na, N), u32_k53(ca), lds, a.L);
+                if (t + 1 < a.T) changed |= table_update_lds(P, philox_node<KIND>(nb, N), u32_k53(cb), lds, a.L);
             }
         }
         uint64_t out[W];
@@ -217,7 +259,7 @@ __global__ __launch_bounds__(SB) void k_rollout(StepArgs a) {
         bool diff = false;  // whole env, only if it differs (see k_step_single)
 #pragma unroll
         for (int k = 0; k < W; ++k) diff |= out[k] != cur[k];
-        if (changed && diff) store_state<W>(a.state + e * W, out);
+        if (live && changed && diff) store_state<W>(a.state + e * W, out);
 #pragma unroll
         for (int k = 0; k < W; ++k) cur[k] = nxt[k];
         e = en;
@@ -377,10 +419,10 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         const uint4* g = reinterpret_cast<const uint4*>(a.img);
         uint4* l = reinterpret_cast<uint4*>(lds);
         // the thresholds ([0, off_rec) of a predictor-mix image) re-expressed on the draw word a
-        // (env_threshold), so the choice compares a itself: no k53 to build per draw
+        // (u32_threshold), so the choice compares a itself: no k53 to build per draw
         for (uint32_t k = threadIdx.x; k < a.L.off_rec / 16; k += BLOCK) {
             const ulonglong2 v = reinterpret_cast<const ulonglong2*>(g)[k];
-            reinterpret_cast<ulonglong2*>(l)[k] = make_ulonglong2(env_threshold(v.x), env_threshold(v.y));
+            reinterpret_cast<ulonglong2*>(l)[k] = make_ulonglong2(u32_threshold(v.x), u32_threshold(v.y));
         }
         const uint32_t tail = a.off_cubes - a.erec_shift;  // the cubes' offset in the device image
         for (uint32_t k = threadIdx.x; k < (a.L.bytes - tail) / 16; k += BLOCK)
@@ -665,7 +707,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 philox_draw(a.seed, used >> 1, a.call_idx + t, g, STREAM_ENV, w);
                 const bool odd = (used & 1u) != 0u;
                 i = philox_node<KIND>(odd ? w[2] : w[0], N);
-                k53 = env_k53(odd ? w[3] : w[1]);
+                k53 = u32_k53(odd ? w[3] : w[1]);
             }
             uint32_t changed;
             if constexpr (KIND == KIND_PREDICTOR_MIX)
@@ -973,7 +1015,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
         uint32_t w4[4];
         philox_draw(a.seed, (used + k) >> 1, a.call_idx + t, gid, STREAM_ENV, w4);
         const uint32_t i = philox_node<KIND_PREDICTOR_MIX>((k & 1u) ? w4[2] : w4[0], N);
-        const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, env_k53((k & 1u) ? w4[3] : w4[1]), lds, a.L)];
+        const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, u32_k53((k & 1u) ? w4[3] : w4[1]), lds, a.L)];
         const uint2 nd = ndelta[i];
         const uint32_t in[4] = {(uint32_t)rec & 0xFFFFu, (uint32_t)(rec >> 16) & 0xFFFFu,
                                 (uint32_t)(rec >> 32) & 0xFFFFu, i};
@@ -1105,11 +1147,10 @@ __global__ __launch_bounds__(BLOCK) void k_rollout_grp(StepArgs a) {
         wave_sync();
         const uint64_t g = a.env_base + e;
         for (uint32_t used = 0; used < a.T; used += G) {
-            const uint64_t u = a.update_base + used + k;
-            uint32_t w4[4];
-            philox_draw(a.seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w4);
-            const uint32_t i = philox_node<KIND_PREDICTOR_MIX>(w4[0], N);
-            const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, k53_of(w4[1], w4[2]), lds, a.L)];
+            uint32_t nw, cw;
+            step_words(a.seed, a.update_base + used + k, g, nw, cw);
+            const uint32_t i = philox_node<KIND_PREDICTOR_MIX>(nw, N);
+            const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, u32_k53(cw), lds, a.L)];
             const uint32_t in[4] = {(uint32_t)rec & 0xFFFFu, (uint32_t)(rec >> 16) & 0xFFFFu,
                                     (uint32_t)(rec >> 32) & 0xFFFFu, i};
             uint32_t v[4];

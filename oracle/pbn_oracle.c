@@ -224,8 +224,8 @@ static inline int philox_node(const orc_net *n, uint32_t w0) {
 
 static inline uint64_t philox_k53(const uint32_t w[4]) { return ((uint64_t)(w[1] >> 5) << 26) | (w[2] >> 6); }
 /* R6 env stream (STREAM_ENV): update u takes Philox call u >> 1, node from word 2(u & 1), the
- * predictor-choice uniform from word 2(u & 1) + 1 as k53 = a << 21 | a >> 11 (pbn_device.hpp env_k53) */
-static inline uint64_t env_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
+ * predictor-choice uniform from word 2(u & 1) + 1 as k53 = a << 21 | a >> 11 (pbn_device.hpp u32_k53) */
+static inline uint64_t u32_k53(uint32_t a) { return ((uint64_t)a << 21) | (uint64_t)(a >> 11); }
 
 /* --------------------------------------------------------------- step modes */
 /* Replay: node_idx/k53 are [T][B] (the draws the reference made). */
@@ -242,7 +242,9 @@ EXPORT int orc_step_replay(const orc_net *n, uint64_t *state, int64_t B, const u
 }
 
 /* Philox: update u (global batch counter) of env with global id g draws
- * philox(key=seed, ctr={u_lo, u_hi, g_lo, g_hi|STEP<<24}). */
+ * philox(key=seed, ctr={u_lo, u_hi, (g>>1)_lo, (g>>1)_hi|STEP<<24}) -- envs 2m and 2m + 1 share
+ * the call -- and takes words 2(g & 1) (node) and 2(g & 1) + 1 (choice, u32_k53)
+ * (pbn_device.hpp step_words). */
 EXPORT int orc_step_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_t seed, uint64_t env_base,
                            uint64_t update_base, int T, int n_threads) {
     const int W = n->n_words;
@@ -257,8 +259,9 @@ EXPORT int orc_step_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_
         for (int t = 0; t < T; t++) {
             uint64_t u = update_base + (uint64_t)t;
             uint32_t w[4];
-            philox_draw(seed, (uint32_t)u, (uint32_t)(u >> 32), g, STREAM_STEP, w);
-            node_update(n, s, philox_node(n, w[0]), philox_k53(w));
+            philox_draw(seed, (uint32_t)u, (uint32_t)(u >> 32), g >> 1, STREAM_STEP, w);
+            const int h = (int)(g & 1u);
+            node_update(n, s, philox_node(n, w[2 * h]), u32_k53(w[2 * h + 1]));
         }
         memcpy(state + e * W, s, 8 * (size_t)W);
     }
@@ -422,7 +425,7 @@ EXPORT int orc_env_step_multi(const orc_net *n, const orc_envcfg *c, uint64_t *s
                 philox_draw(seed, used >> 1, call_idx, env_base + (uint64_t)e, STREAM_ENV, w);
                 const int h = (int)(used & 1u);
                 i = philox_node(n, w[2 * h]);
-                k53 = env_k53(w[2 * h + 1]);
+                k53 = u32_k53(w[2 * h + 1]);
             }
             node_update(n, s, i, k53);
             used++;
