@@ -334,25 +334,40 @@ def r6_supplement(args, world, rank, device, dist, valu):
     v = torch.randint(1, net.n_nodes + 1, (T, B, A), device=dev, generator=g, dtype=torch.int32)
     acts = (v * (torch.rand((T, B, A), device=dev, generator=g) >= 0.75)).to(torch.int32).contiguous()
 
+    def chunk_stats(buf):
+        # per env step: the slowest env (a per-step launch waits for it) and the mean; capped envs
+        n = buf["n_updates"]
+        return n.to(torch.int64).sum(), torch.stack([n.max(dim=1).values.to(torch.float64),
+                                                     n.to(torch.float64).mean(dim=1),
+                                                     ((buf["flags"] & 4) != 0).to(torch.float64).mean(dim=1)])
+
     def run(fused):
         b = PBNBatch(net, B, device=device, env_id_base=sh.env_base, seed=0xAC7)
         col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=CAP, dist=dist, fused=fused)
-        col.step_chunk(acts)  # warm-up chunk
+
+        def chunks():
+            ups = torch.zeros((), dtype=torch.int64, device=dev)
+            stats = []
+            for _ in range(args.r6_chunks):
+                buf, _ = col.step_chunk(acts)
+                u, st = chunk_stats(buf)
+                ups += u
+                stats.append(st)
+            return buf, ups, stats
+
+        # warm-up: the timed loop itself, untimed, with the per-launch events on -- the first use
+        # of the events (created on demand, then reused) and of torch's small kernels costs tens
+        # of ms, which otherwise landed in the first timed per-step chunks (48-79 vs 97 M env-steps/s)
+        b.timing(1)
+        chunks()
+        b.timing(0)
         col.finish()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        ups = torch.zeros((), dtype=torch.int64, device=dev)
-        stats = []
         b.timing(1)  # an event pair around every launch on the batch stream: kernel time alone
         t0 = time.perf_counter()
-        for _ in range(args.r6_chunks):
-            buf, _ = col.step_chunk(acts)
-            n = buf["n_updates"]
-            ups += n.to(torch.int64).sum()
-            # per env step: the slowest env (a per-step launch waits for it) and the mean; capped envs
-            stats.append(torch.stack([n.max(dim=1).values.to(torch.float64), n.to(torch.float64).mean(dim=1),
-                                      ((buf["flags"] & 4) != 0).to(torch.float64).mean(dim=1)]))
+        buf, ups, stats = chunks()
         col.finish()
         torch.cuda.synchronize()
         if dist is not None:
