@@ -52,9 +52,12 @@ def test_single_env_b1_plumbing(G):
 
 
 # ----------------------------------------------------------------- Philox mode vs oracle
+# an even env base puts envs 2m / 2m + 1 (which share a Philox call) in lane pairs that swap words
+# over DPP; an odd base takes the one-call-per-env path
+@pytest.mark.parametrize("base", [77, 64])
 @pytest.mark.parametrize("name,B,T", [("bittner28", 4096, 64), ("bittner199", 8192, 40), ("tt200", 4096, 40),
-                                      ("bittner70", 3000, 33), ("tt8", 1000, 50), ("syn500", 2048, 24)])
-def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
+                                      ("bittner70", 3001, 33), ("tt8", 1000, 50), ("syn500", 2048, 24)])
+def test_philox_step_matches_oracle(G, oracle_mod, name, B, T, base):
     if name == "syn500":  # W = 8 state words: the largest network the build takes (N <= 512)
         from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
 
@@ -63,14 +66,14 @@ def test_philox_step_matches_oracle(G, oracle_mod, name, B, T):
     else:
         net = load_network(name)
     o = oracle_mod.Oracle(net)
-    b = G.PBNBatch(net, B, seed=1234, env_id_base=77)
+    b = G.PBNBatch(net, B, seed=1234, env_id_base=base)
     b.randomize()
     init = b.get_state()
-    assert np.array_equal(init, o.init_philox(B, seed=1234, env_base=77))
+    assert np.array_equal(init, o.init_philox(B, seed=1234, env_base=base))
     b.step(T)  # T launches, one update each
-    assert np.array_equal(b.get_state(), o.step_philox(init, 1234, 77, 0, T))
-    b.rollout(T)  # T updates in registers, counters continue
-    assert np.array_equal(b.get_state(), o.step_philox(init, 1234, 77, 0, 2 * T))
+    assert np.array_equal(b.get_state(), o.step_philox(init, 1234, base, 0, T))
+    b.rollout(T)  # T updates in registers, counters continue (odd T: the last pair half-used)
+    assert np.array_equal(b.get_state(), o.step_philox(init, 1234, base, 0, 2 * T))
 
 
 @pytest.mark.parametrize("graph", ["1", "0"])
@@ -107,20 +110,22 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
     b.close()
 
 
+@pytest.mark.parametrize("base", [9, 10])
 @pytest.mark.parametrize("k", ["1", "2", "4", "8"])
 @pytest.mark.parametrize("name,B", [("bittner199", 70001), ("bittner28", 300001), ("tt200", 40000)])
-def test_envs_per_thread_match_oracle(G, oracle_mod, monkeypatch, k, name, B):
+def test_envs_per_thread_match_oracle(G, oracle_mod, monkeypatch, k, name, B, base):
     """Step mode with 1, 2, 4 or 8 envs per thread (the grid-stride pairs of k_step_single): ragged
-    batches, every env against the oracle, graph-replayed and plain launches."""
+    batches (the last env's DPP partner lane has left the loop), odd and even env bases, every env
+    against the oracle, graph-replayed and plain launches."""
     monkeypatch.setenv("PBNSIM_ENVS_PER_THREAD", k)
     net = load_network(name)
     o = oracle_mod.Oracle(net)
-    b = G.PBNBatch(net, B, seed=404, env_id_base=9)
+    b = G.PBNBatch(net, B, seed=404, env_id_base=base)
     b.randomize()
     init = b.get_state()
     b.step(3)
     b.step(1)
-    assert np.array_equal(b.get_state(), o.step_philox(init, 404, 9, 0, 4))
+    assert np.array_equal(b.get_state(), o.step_philox(init, 404, base, 0, 4))
     b.close()
 
 
