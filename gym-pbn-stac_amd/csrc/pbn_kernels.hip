@@ -405,6 +405,15 @@ __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01
 
 constexpr uint32_t ENV_OWN_DRAWS_MIN = 40;  // active lanes from which a wave skips the shared draw tables
 
+// ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
+struct RankMagic {
+    uint32_t v[64];
+    constexpr RankMagic() : v{} {
+        for (uint32_t n = 2; n < 64; ++n) v[n] = (uint32_t)((0x100000000ull + n - 1) / n);
+    }
+};
+__constant__ constexpr RankMagic kRankMagic{};
+
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     constexpr bool GEN = FAST == 2 || FAST == 4;
@@ -565,7 +574,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             const uint32_t total = nact * (ENV_CHUNK / 2);  // pairs of updates: one Philox call each
             // k / nact as a multiply-high by ceil(2^32 / nact): exact for k < 2^16 (nact == 1 handled apart,
             // its multiplier 2^32 does not fit 32 bits)
-            const uint32_t magic = nact > 1 ? (uint32_t)((0x100000000ull + nact - 1) / nact) : 0u;
+            const uint32_t magic = kRankMagic.v[nact];  // a 64-bit divide here was ~120 scalar instructions
             for (uint32_t k0 = 0; k0 < total; k0 += 64) {
                 const uint32_t k = k0 + lane;
                 if (k < total) {
