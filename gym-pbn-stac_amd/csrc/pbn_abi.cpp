@@ -280,6 +280,10 @@ static int build_predictor_image(const pbn_net_desc* d, pbn_net* n) {
     L.off_thr = 0;
     L.off_rec = align16(8u * L.tp * (uint32_t)N);
     L.bytes = align16(L.off_rec + 8u * pmax * (uint32_t)N);
+    {  // the Philox kernels' compact LDS image (thr32_layout, pbn_device.hpp) fits the same budget
+        const uint32_t tp4 = (L.tp + 3u) & ~3u, rs = std::max(tp4 + 1u, pmax);
+        L.bytes = std::max(L.bytes, align16(align16(4u * tp4 * (uint32_t)N) + 8u * rs * (uint32_t)N));
+    }
     L.kind = KIND_PREDICTOR_MIX;
     L.n_nodes = N;
     if (L.bytes > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "network tables (%u B) exceed the LDS budget", L.bytes);
@@ -298,6 +302,32 @@ static int build_predictor_image(const pbn_net_desc* d, pbn_net* n) {
                            ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 1] << 16) |
                            ((uint64_t)(uint32_t)d->pred_inputs[3 * j + 2] << 32) | ((uint64_t)d->pred_tt[j] << 48);
             memcpy(im + L.off_rec + 8 * ((size_t)i * pmax + q), &rec, 8);
+        }
+    }
+    // Compact image of the Philox kernels, appended after L.bytes (thr32_layout / stage_image_thr32
+    // in pbn_device.hpp): u32 thresholds on the choice word, saturated; slot tp4 of a node's record
+    // row holds the record a = 2^32 - 1 selects (its count of thresholds below 2^32), which is where
+    // the saturated count lands.
+    const uint32_t tp4 = (L.tp + 3u) & ~3u, rs = std::max(tp4 + 1u, pmax);
+    const uint32_t rec_off = align16(4u * tp4 * (uint32_t)N);
+    n->image.resize((size_t)L.bytes + align16(rec_off + 8u * rs * (uint32_t)N), 0);
+    im = n->image.data();  // resize reallocates
+    uint8_t* cm = im + L.bytes;
+    auto k53 = [](uint64_t a) { return (a << 21) | (a >> 11); };
+    for (int i = 0; i < N; i++) {
+        uint32_t m = 0;
+        for (uint32_t q = 0; q < tp4; q++) {
+            uint64_t T = ~0ull;
+            if (q < L.tp) memcpy(&T, im + L.off_thr + 8 * ((size_t)i * L.tp + q), 8);
+            const uint64_t a0 = T >> 21;
+            const uint64_t t = a0 >= (1ull << 32) ? (1ull << 32) : (k53(a0) >= T ? a0 : a0 + 1u);
+            m += t >> 32 ? 0u : 1u;
+            const uint32_t s = t >> 32 ? 0xFFFFFFFFu : (uint32_t)t;
+            memcpy(cm + 4 * ((size_t)i * tp4 + q), &s, 4);
+        }
+        for (uint32_t q = 0; q < rs; q++) {
+            const uint32_t src = q == tp4 ? m : q;
+            if (src < pmax) memcpy(cm + rec_off + 8 * ((size_t)i * rs + q), im + L.off_rec + 8 * ((size_t)i * pmax + src), 8);
         }
     }
     n->L = L;
@@ -1140,7 +1170,7 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
         return fail(PBN_E_UNSUPPORTED, "network + %d attractor cubes exceed the LDS budget", d->n_cubes);
     }
     c->image.assign(bytes, 0);
-    memcpy(c->image.data(), net->image.data(), net->image.size());
+    memcpy(c->image.data(), net->image.data(), net->L.bytes);  // not the compact image appended after it
     uint64_t* cubes = reinterpret_cast<uint64_t*>(c->image.data() + c->off_cubes);
     for (int h = 0; h < c->H; h++)
         for (int k = 0; k < W; k++) {

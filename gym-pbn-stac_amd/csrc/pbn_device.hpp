@@ -229,6 +229,48 @@ __device__ __forceinline__ uint64_t predictor_record(uint32_t i, uint64_t k53, c
     return reinterpret_cast<const uint64_t*>(tbl + L.off_rec)[i * L.pmax + predictor_choice(i, k53, tbl, L)];
 }
 
+// Compact LDS image of the Philox-driven predictor-mix kernels (k_step, k_rollout), whose choice
+// uniform is a 32-bit word a (k53 = u32_k53(a)): thresholds re-expressed on a (u32_threshold)
+// and stored as u32, rows padded to tp4 (a multiple of 4) so one ds_read_b128 serves 4 of them
+// -- half the LDS bytes of the u64 thresholds, whose random-node reads are the most
+// bank-conflicted reads of an update. u32_threshold can be 2^32 ("never": the u64 padding, or
+// a threshold above k53(2^32 - 1)); it is stored saturated to 2^32 - 1, which a = 2^32 - 1
+// passes. Thresholds are non-decreasing, so the never-entries of a node are its last tp - m_i;
+// record slots q >= m_i all hold record m_i (slot rs >= tp4 + 1 per node), and the count's
+// overshoot at a = 2^32 - 1 lands on the same record. Bit-exact with predictor_record(i, u32_k53(a)).
+// Layout: thr32 [N][tp4] at 0, records u64 [N][rs] at rec_off (16-aligned); never larger than
+// the u64 image's L.bytes (the host pads L.bytes to cover it). The host builds it
+// (build_predictor_image, pbn_abi.cpp) and appends it to the device image at offset L.bytes.
+struct Thr32 {
+    uint32_t tp4, rs, rec_off, bytes;
+};
+
+__device__ __forceinline__ Thr32 thr32_layout(const NetLayout& L) {
+    Thr32 X;
+    X.tp4 = (L.tp + 3u) & ~3u;
+    X.rs = X.tp4 + 1u > L.pmax ? X.tp4 + 1u : L.pmax;
+    X.rec_off = ((uint32_t)L.n_nodes * X.tp4 * 4u + 15u) & ~15u;
+    X.bytes = (X.rec_off + (uint32_t)L.n_nodes * X.rs * 8u + 15u) & ~15u;
+    return X;
+}
+
+__device__ __forceinline__ uint64_t predictor_record32(uint32_t i, uint32_t a, const uint8_t* lds,
+                                                       const Thr32& X) {
+    const uint4* thr = reinterpret_cast<const uint4*>(lds) + i * (X.tp4 >> 2);
+    uint32_t j = 0;
+    if (X.tp4 == 4) {
+        const uint4 t = thr[0];
+        j = (a >= t.x ? 1u : 0u) + (a >= t.y ? 1u : 0u) + (a >= t.z ? 1u : 0u) + (a >= t.w ? 1u : 0u);
+    } else {
+#pragma unroll 4
+        for (uint32_t q = 0; q < (X.tp4 >> 2); ++q) {
+            const uint4 t = thr[q];
+            j += (a >= t.x ? 1u : 0u) + (a >= t.y ? 1u : 0u) + (a >= t.z ? 1u : 0u) + (a >= t.w ? 1u : 0u);
+        }
+    }
+    return reinterpret_cast<const uint64_t*>(lds + X.rec_off)[i * X.rs + j];
+}
+
 // Y = rec.tt[x_in0 x_in1 x_in2 x_self] (base.py:100-118 via the exported truth table).
 template <class P_t>
 __device__ __forceinline__ uint32_t predictor_apply(const P_t& P, uint32_t i, uint32_t self, uint64_t rec) {

@@ -67,20 +67,26 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
         }
         i0 = philox_node<KIND>(n0, N);
         i1 = philox_node<KIND>(n1, N);
-        q0 = u32_k53(c0);
-        q1 = u32_k53(c1);
+        // predictor mix: the choice word itself (compact image, thresholds on the word); tables: k53
+        q0 = KIND == KIND_PREDICTOR_MIX ? (uint64_t)c0 : u32_k53(c0);
+        q1 = KIND == KIND_PREDICTOR_MIX ? (uint64_t)c1 : u32_k53(c1);
     };
     if (e + po < a.B) load_state<W>(a.state + (e + po) * W, nxt);
     draws(e);
-    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    const Thr32 X = thr32_layout(a.L);
+    if constexpr (KIND == KIND_PREDICTOR_MIX)  // the compact image (thresholds on the choice word)
+        stage_image(reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.img) + a.L.bytes), X.bytes / 16,
+                    reinterpret_cast<uint4*>(lds));
+    else
+        stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     while (e < a.B) {
         const uint64_t e1 = e + po;
         uint64_t r0 = 0, r1 = 0;
         if constexpr (KIND == KIND_PREDICTOR_MIX) {  // state-independent: before the loads land
-            r0 = predictor_record(i0, q0, lds, a.L);
-            r1 = predictor_record(i1, q1, lds, a.L);
+            r0 = predictor_record32(i0, (uint32_t)q0, lds, X);
+            r1 = predictor_record32(i1, (uint32_t)q1, lds, X);
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -180,7 +186,12 @@ __global__ __launch_bounds__(SB) void k_rollout(StepArgs a) {
     const uint32_t N = (uint32_t)a.L.n_nodes;
     uint64_t cur[W];
     if (e < a.B) load_state<W>(a.state + e * W, cur);
-    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    const Thr32 X = thr32_layout(a.L);
+    if constexpr (KIND == KIND_PREDICTOR_MIX)  // the compact image (thresholds on the choice word)
+        stage_image(reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.img) + a.L.bytes), X.bytes / 16,
+                    reinterpret_cast<uint4*>(lds));
+    else
+        stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     // Envs 2m / 2m + 1 share their Philox calls (pbn_device.hpp). With an even env base the lane
@@ -227,8 +238,8 @@ __global__ __launch_bounds__(SB) void k_rollout(StepArgs a) {
                 words2(t, na, ca, nb, cb);
                 ia = philox_node<KIND>(na, N);
                 ib = philox_node<KIND>(nb, N);
-                ra = predictor_record(ia, u32_k53(ca), lds, a.L);
-                rb = predictor_record(ib, u32_k53(cb), lds, a.L);
+                ra = predictor_record32(ia, ca, lds, X);
+                rb = predictor_record32(ib, cb, lds, X);
             };
             auto apply = [&](uint32_t i, uint64_t rec) {
                 const uint32_t d = i >> 5, sh = i & 31u;
