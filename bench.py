@@ -506,7 +506,9 @@ def main():
     batch.step(args.warmup)
     batch.prepare_steps(args.steps)  # setup, nothing runs (graph capture where the batch uses graphs)
     batch.sync()
-    time.sleep(0.005)  # idle gap: the timed launches are a run of their own in a kernel trace
+    # no idle gap before the timed launches: a 5 ms sleep added ~0.4 us per timed launch to the wall
+    # clock, a 0.2 ms busy wait ~0.2 us (tools/timing_window.py); the host syncs below still leave the
+    # timed run a gap of its own in a kernel trace (tools/trace_split.py)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -514,8 +516,7 @@ def main():
     t0 = time.perf_counter()
     batch.step(args.steps)
     batch.timing(0)  # closes the event region right behind the last launch
-    batch.sync()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # device-wide: covers the batch's own stream (a stream sync first cost ~0.25 us/launch)
     t1 = time.perf_counter()
     barrier()
     kernel_ms, launches = batch.timing_read()

@@ -1531,6 +1531,14 @@ int pbn_timing_enable(pbn_batch* b, int enable) {
         b->timing = enable;
         return 0;
     }
+    if (enable == 2 && b->ev_pool.empty()) {
+        // create the region's event pair now, not at its first launch (inside a timed window)
+        SET_DEV(b);
+        hipEvent_t e0, e1;
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        b->ev_pool.emplace_back(e0, e1);
+    }
     b->timing = enable;
     b->ev_used = 0;
     b->region_launches = 0;

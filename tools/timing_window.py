@@ -20,8 +20,12 @@ def window(net, B, sleep, batch_sync, events, steps=20, warmup=5):
     b.step(warmup)
     b.prepare_steps(steps)
     b.sync()
-    if sleep:
+    if sleep == 1:
         time.sleep(0.005)
+    elif sleep == 2:  # busy wait (bench.py's gap)
+        t = time.perf_counter()
+        while time.perf_counter() - t < 2e-4:
+            pass
     torch.cuda.synchronize()
     if events:
         b.timing(2)
@@ -43,7 +47,8 @@ def main():
     B = 1 << 20
     torch.zeros(1, device="cuda")
     variants = {"bench": (1, 1, 1), "no_sleep": (0, 1, 1), "torch_sync_only": (1, 0, 1),
-                "no_events": (1, 1, 0), "no_sleep_torch_sync_only": (0, 0, 1), "bare": (0, 0, 0)}
+                "no_events": (1, 1, 0), "no_sleep_torch_sync_only": (0, 0, 1), "bare": (0, 0, 0),
+                "spin_torch_sync_only (bench.py now)": (2, 0, 1)}
     res = {k: [] for k in variants}
     for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 7):
         for k, v in variants.items():

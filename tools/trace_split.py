@@ -6,8 +6,8 @@ supplement, the headline's warm-up + timed launches and the twin batch that meas
 fraction, so the --stats average mixes sizes. A run = consecutive dispatches of the kernel whose
 start follows the previous end by less than --gap microseconds. Prints one JSON object: every
 run's launch count, mean / min / max duration (us) and first dispatch id; the headline's K timed
-launches are the run of length K right after its W warm-up launches (bench.py leaves the GPU idle
-for a few ms between the two, so they are separate runs).
+launches are the run of length K right after its W warm-up launches (the host syncs between the
+two leave the GPU idle for tens of microseconds, so they are separate runs at the default gap).
 
 Usage: trace_split.py <kernel_trace.csv> [--kernel SUBSTR] [--gap US] [--min-launches N]
 """
@@ -20,7 +20,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("trace")
     p.add_argument("--kernel", default="k_step<4, 1, 1, 0, 1024>")
-    p.add_argument("--gap", type=float, default=50.0)
+    p.add_argument("--gap", type=float, default=10.0)
     p.add_argument("--min-launches", type=int, default=2, help="runs shorter than this are left out")
     a = p.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
