@@ -1134,10 +1134,11 @@ __global__ __launch_bounds__(BLOCK) void k_env_grp(EnvArgs a) {
 template <int W, int G>
 __global__ __launch_bounds__(BLOCK) void k_rollout_grp(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
-    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    const Thr32 X = thr32_layout(a.L);  // the compact image (thresholds on the choice word)
+    stage_image(reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.img) + a.L.bytes), X.bytes / 16,
+                reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const uint32_t N = (uint32_t)a.L.n_nodes;
-    const uint64_t* recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
     const uint32_t lane = __lane_id();
     const uint32_t k = lane & (G - 1);
     const uint32_t gbase = lane & ~(uint32_t)(G - 1);
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout_grp(StepArgs a) {
             uint32_t nw, cw;
             step_words(a.seed, a.update_base + used + k, g, nw, cw);
             const uint32_t i = philox_node<KIND_PREDICTOR_MIX>(nw, N);
-            const uint64_t rec = recs[i * a.L.pmax + predictor_choice(i, u32_k53(cw), lds, a.L)];
+            const uint64_t rec = predictor_record32(i, cw, lds, X);
             const uint32_t in[4] = {(uint32_t)rec & 0xFFFFu, (uint32_t)(rec >> 16) & 0xFFFFu,
                                     (uint32_t)(rec >> 32) & 0xFFFFu, i};
             uint32_t v[4];
