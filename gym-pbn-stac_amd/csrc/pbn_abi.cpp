@@ -1313,7 +1313,9 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     // (pbn_device.hpp env_record): the tables after them move up by erec_shift
     uint32_t erec_shift = 0;
     if (mode == 2) {
-        const uint32_t nrec = (uint32_t)b->net->N * cfg->L.pmax;
+        // rows of rs records (thr32_layout: tp4 + 1 slots at least, for the saturated choice)
+        const uint32_t tp4 = (cfg->L.tp + 3u) & ~3u;
+        const uint32_t nrec = (uint32_t)b->net->N * std::max(tp4 + 1u, cfg->L.pmax);
         erec_shift = cfg->L.off_rec + 16u * nrec - cfg->off_cubes;
         if (nrec > 65535u || env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1) > 64u * 1024u) {
             mode = cfg->fast;  // too large for the u16 record index / one workgroup's LDS

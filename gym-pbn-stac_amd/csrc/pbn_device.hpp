@@ -254,21 +254,26 @@ __device__ __forceinline__ Thr32 thr32_layout(const NetLayout& L) {
     return X;
 }
 
-__device__ __forceinline__ uint64_t predictor_record32(uint32_t i, uint32_t a, const uint8_t* lds,
-                                                       const Thr32& X) {
-    const uint4* thr = reinterpret_cast<const uint4*>(lds) + i * (X.tp4 >> 2);
+// Record slot of node i's row chosen by the choice word a (compact thresholds at lds[0]).
+__device__ __forceinline__ uint32_t predictor_choice32(uint32_t i, uint32_t a, const uint8_t* lds, uint32_t tp4) {
+    const uint4* thr = reinterpret_cast<const uint4*>(lds) + i * (tp4 >> 2);
     uint32_t j = 0;
-    if (X.tp4 == 4) {
+    if (tp4 == 4) {
         const uint4 t = thr[0];
         j = (a >= t.x ? 1u : 0u) + (a >= t.y ? 1u : 0u) + (a >= t.z ? 1u : 0u) + (a >= t.w ? 1u : 0u);
     } else {
 #pragma unroll 4
-        for (uint32_t q = 0; q < (X.tp4 >> 2); ++q) {
+        for (uint32_t q = 0; q < (tp4 >> 2); ++q) {
             const uint4 t = thr[q];
             j += (a >= t.x ? 1u : 0u) + (a >= t.y ? 1u : 0u) + (a >= t.z ? 1u : 0u) + (a >= t.w ? 1u : 0u);
         }
     }
-    return reinterpret_cast<const uint64_t*>(lds + X.rec_off)[i * X.rs + j];
+    return j;
+}
+
+__device__ __forceinline__ uint64_t predictor_record32(uint32_t i, uint32_t a, const uint8_t* lds,
+                                                       const Thr32& X) {
+    return reinterpret_cast<const uint64_t*>(lds + X.rec_off)[i * X.rs + predictor_choice32(i, a, lds, X.tp4)];
 }
 
 // Y = rec.tt[x_in0 x_in1 x_in2 x_self] (base.py:100-118 via the exported truth table).

@@ -432,24 +432,39 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     static_assert(!GEN || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
     extern __shared__ __align__(16) uint8_t lds[];
     const uint32_t N = (uint32_t)a.L.n_nodes;
+    const Thr32 X = thr32_layout(a.L);
     if constexpr (GEN) {
         // LDS: the thresholds as staged; in place of the 8-B predictor records, 16-B "env
         // records" (EnvRec) carrying each input's plane offset and bit position, so an update
         // does no index arithmetic; the cubes / target / deltas after them move up by erec_shift
         const uint4* g = reinterpret_cast<const uint4*>(a.img);
         uint4* l = reinterpret_cast<uint4*>(lds);
-        // the thresholds ([0, off_rec) of a predictor-mix image) re-expressed on the draw word a
-        // (u32_threshold), so the choice compares a itself: no k53 to build per draw
-        for (uint32_t k = threadIdx.x; k < a.L.off_rec / 16; k += BLOCK) {
-            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(g)[k];
-            reinterpret_cast<ulonglong2*>(l)[k] = make_ulonglong2(u32_threshold(v.x), u32_threshold(v.y));
+        // the thresholds re-expressed on the draw word a as the compact image has them (u32, rows
+        // of tp4, saturated: thr32_layout), so the choice compares a itself in one 16-B read; env
+        // records in rows of rs, slot tp4 holding the record a = 2^32 - 1 selects. Staged once
+        // per persistent workgroup, so this computes the conversion instead of reading the
+        // compact image (the env config's image does not carry it)
+        const uint64_t* gthr = reinterpret_cast<const uint64_t*>(a.img);
+        const uint32_t tp = a.L.tp, tp4 = X.tp4, rs = X.rs;
+        for (uint32_t k = threadIdx.x; k < N * tp4; k += BLOCK) {
+            const uint32_t i = k / tp4, q = k - i * tp4;
+            const uint64_t t = q < tp ? u32_threshold(gthr[i * tp + q]) : (1ull << 32);
+            reinterpret_cast<uint32_t*>(lds)[k] = t >> 32 ? 0xFFFFFFFFu : (uint32_t)t;
         }
         const uint32_t tail = a.off_cubes - a.erec_shift;  // the cubes' offset in the device image
         for (uint32_t k = threadIdx.x; k < (a.L.bytes - tail) / 16; k += BLOCK)
             l[(tail + a.erec_shift) / 16 + k] = g[tail / 16 + k];
         const uint64_t* grec = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(a.img) + a.L.off_rec);
         uint4* erec = reinterpret_cast<uint4*>(lds + a.L.off_rec);
-        for (uint32_t r = threadIdx.x; r < N * a.L.pmax; r += BLOCK) erec[r] = env_record(grec[r], r / a.L.pmax);
+        for (uint32_t r = threadIdx.x; r < N * rs; r += BLOCK) {
+            const uint32_t i = r / rs, q = r - i * rs;
+            uint32_t src = q;
+            if (q == tp4) {  // the node's thresholds below 2^32 on a (a prefix: non-decreasing)
+                src = 0;
+                for (uint32_t p = 0; p < tp; ++p) src += (u32_threshold(gthr[i * tp + p]) >> 32) ? 0u : 1u;
+            }
+            erec[r] = env_record(src < a.L.pmax ? grec[i * a.L.pmax + src] : 0ull, i);
+        }
     } else {
         stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     }
@@ -568,8 +583,8 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
                     for (uint32_t h = 0; h < 2; ++h) {
                         const uint32_t i = philox_node<KIND>(w[2 * h], N);
-                        const uint32_t j = predictor_choice(i, (uint64_t)w[2 * h + 1], lds, a.L);
-                        gbuf[(sl + h) * 64 + lane] = (uint16_t)(__umul24(i, a.L.pmax) + j);  // EnvRec index
+                        const uint32_t j = predictor_choice32(i, w[2 * h + 1], lds, X.tp4);
+                        gbuf[(sl + h) * 64 + lane] = (uint16_t)(__umul24(i, X.rs) + j);  // EnvRec index
                     }
                 }
             } else {
@@ -596,8 +611,8 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 #pragma unroll
                     for (uint32_t h = 0; h < 2; ++h) {
                         const uint32_t i = philox_node<KIND>(w[2 * h], N);
-                        const uint32_t j = predictor_choice(i, (uint64_t)w[2 * h + 1], lds, a.L);
-                        gbuf[(2 * sp + h) * 64 + q] = (uint16_t)(__umul24(i, a.L.pmax) + j);
+                        const uint32_t j = predictor_choice32(i, w[2 * h + 1], lds, X.tp4);
+                        gbuf[(2 * sp + h) * 64 + q] = (uint16_t)(__umul24(i, X.rs) + j);
                     }
                 }
             }
