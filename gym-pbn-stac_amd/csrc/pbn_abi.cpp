@@ -428,6 +428,25 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     return 0;
 }
 
+int pbn_net_select_u32(const pbn_net* n, int32_t node, uint32_t a, uint64_t* record) {
+    CHECK_NN(n, "net");
+    CHECK_NN(record, "record");
+    if (n->L.kind != KIND_PREDICTOR_MIX) return fail(PBN_E_INVALID, "not a predictor-mix network");
+    if (node < 0 || node >= n->L.n_nodes) return fail(PBN_E_RANGE, "node %d out of range", node);
+    // thr32_layout / predictor_choice32 / predictor_record32 (pbn_device.hpp) on the host copy
+    const uint32_t tp4 = (n->L.tp + 3u) & ~3u, rs = std::max(tp4 + 1u, n->L.pmax);
+    const uint32_t rec_off = align16(4u * tp4 * (uint32_t)n->L.n_nodes);
+    const uint8_t* cm = n->image.data() + n->L.bytes;
+    uint32_t j = 0;
+    for (uint32_t q = 0; q < tp4; q++) {
+        uint32_t t;
+        memcpy(&t, cm + 4 * ((size_t)node * tp4 + q), 4);
+        j += a >= t ? 1u : 0u;
+    }
+    memcpy(record, cm + rec_off + 8 * ((size_t)node * rs + j), 8);
+    return 0;
+}
+
 void pbn_net_destroy(pbn_net* n) {
     if (!n) return;
     for (auto& kv : n->dev_image) {

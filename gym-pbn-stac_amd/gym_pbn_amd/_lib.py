@@ -85,6 +85,7 @@ SIGNATURES = {
     "pbn_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "pbn_net_create": (C.c_int, [C.POINTER(NetDesc), _PP]),
     "pbn_net_destroy": (None, [_vp]),
+    "pbn_net_select_u32": (C.c_int, [_vp, C.c_int32, C.c_uint32, _u64p]),
     "pbn_batch_create": (C.c_int, [_vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, _PP]),
     "pbn_batch_destroy": (None, [_vp]),
     "pbn_batch_get_info": (C.c_int, [_vp, C.POINTER(BatchInfo)]),

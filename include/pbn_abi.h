@@ -124,6 +124,12 @@ int pbn_device_count(int *count);
 /* ---- networks: replaces graph construction, bittner/utils.py:81-91 / pbn.py:78-87 ---- */
 int pbn_net_create(const pbn_net_desc *desc, pbn_net **out);
 void pbn_net_destroy(pbn_net *net);
+/* Predictor-mix networks: the predictor record (in0 | in1<<16 | in2<<32 | tt<<48) that choice
+ * word a selects for node `node`, read from the compact image the Philox kernels stage (u32
+ * thresholds, saturated, overshoot slot) by the kernels' own rule -- host side, no device. For
+ * tests: equals the record of predictor min(#{q : u32_k53(a) >= thr_q}, count - 1)
+ * (Predstep's choice, base.py:94-97). */
+int pbn_net_select_u32(const pbn_net *net, int32_t node, uint32_t a, uint64_t *record);
 
 /* ---- batches of independent envs (the reference holds one Graph per env) ---- */
 /* Tuning knobs, read from the environment once here (measurement and tests only):
