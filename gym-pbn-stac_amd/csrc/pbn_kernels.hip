@@ -22,6 +22,12 @@
 
 namespace pbn {
 
+#ifdef PBN_STAMPS
+// Measurement builds only (tools/build_exp.sh -DPBN_STAMPS): per-wave s_memrealtime stamps (100 MHz)
+// of the step kernel's phases, kept in registers and written once at the end of the wave.
+__device__ uint64_t g_stamps[16384 * 8];
+#endif
+
 // ------------------------------------------------------------------ step
 // Layout per workgroup in LDS: [network image][state planes]. The state planes
 // hold, for the env each lane is working on, its 2W dwords in planar order
@@ -41,9 +47,9 @@ namespace pbn {
 // bench sizes every thread owns exactly one pair. The pair's draws and (for predictor
 // networks) its predictor records depend only on (seed, update counter, env id), so
 // they are computed while the pair's state loads are in flight.
-template <int W, int KIND, int STORE, int SB>
+template <int W, int KIND, int STORE, int SB, bool PRE = false>
 __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, uint64_t e, uint64_t stride,
-                                              uint64_t (&cur)[W], uint32_t N) {
+                                              uint64_t (&cur)[W], uint32_t N, uint64_t (*pre_nxt)[W] = nullptr) {
     // graph replays read the batch's update counter from device memory (k_bump advances it)
     const uint64_t u = a.update_base + (a.ubase_dev ? *a.ubase_dev : 0ull);
     const uint64_t po = stride;  // second env of the pair (adjacent envs measured slower: 8.2 vs 7.8 us)
@@ -71,15 +77,30 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
         q0 = KIND == KIND_PREDICTOR_MIX ? (uint64_t)c0 : u32_k53(c0);
         q1 = KIND == KIND_PREDICTOR_MIX ? (uint64_t)c1 : u32_k53(c1);
     };
+#ifdef PBN_STAMPS
+    uint64_t st[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
+#endif
+    const Thr32 X = thr32_layout(a.L);
+    if constexpr (PRE) {  // image staged and both loads issued by the caller (k_step)
+#pragma unroll
+        for (int k = 0; k < W; ++k) nxt[k] = (*pre_nxt)[k];
+        draws(e);
+    } else {
     if (e + po < a.B) load_state<W>(a.state + (e + po) * W, nxt);
     draws(e);
-    const Thr32 X = thr32_layout(a.L);
+#ifdef PBN_STAMPS
+    st[1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if constexpr (KIND == KIND_PREDICTOR_MIX)  // the compact image (thresholds on the choice word)
         stage_image(reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.img) + a.L.bytes), X.bytes / 16,
                     reinterpret_cast<uint4*>(lds));
     else
         stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
+    }
+#ifdef PBN_STAMPS
+    st[2] = __builtin_amdgcn_s_memrealtime();
+#endif
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     while (e < a.B) {
         const uint64_t e1 = e + po;
@@ -88,6 +109,12 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             r0 = predictor_record32(i0, (uint32_t)q0, lds, X);
             r1 = predictor_record32(i1, (uint32_t)q1, lds, X);
         }
+#ifdef PBN_STAMPS
+        if (!st[3]) {
+            __builtin_amdgcn_s_waitcnt(0);  // records read and state landed (measurement build)
+            st[3] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint64_t eh = h ? e1 : e;
@@ -124,6 +151,9 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
                 store_state<W>(a.state + eh * W, out);
             }
         }
+#ifdef PBN_STAMPS
+        if (!st[4]) st[4] = __builtin_amdgcn_s_memrealtime();  // the first pair's stores issued
+#endif
         e += 2 * stride;
         if (e < a.B) {
             load_state<W>(a.state + e * W, cur);
@@ -131,6 +161,16 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             draws(e);
         }
     }
+#ifdef PBN_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    st[5] = __builtin_amdgcn_s_memrealtime();  // every store of the wave done
+    const uint32_t wv = blockIdx.x * (SB / 64) + threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0 && wv < 16384) {
+        st[6] = blockIdx.x;
+        st[7] = __smid();
+        for (int k = 0; k < 8; ++k) g_stamps[wv * 8 + k] = st[k];
+    }
+#endif
 }
 
 // Step mode (T == 1, Philox; REPLAY == 0) and replay mode (REPLAY == 1: T updates from the
@@ -138,12 +178,38 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
 // path's code shapes the other's register allocation and schedule (sharing one kernel cost
 // the step path 0.6 us per launch at 1M envs).
 template <int W, int KIND, int STORE, int REPLAY, int SB>
-__global__ __launch_bounds__(SB) void k_step(StepArgs a) {
+__global__ __launch_bounds__(SB)
+#ifdef PBN_STAMPS
+__attribute__((amdgpu_waves_per_eu(8, 8)))  // the product's occupancy (64 VGPRs) despite the stamps
+#endif
+void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     const uint64_t stride = (uint64_t)gridDim.x * SB;
     uint64_t e = (uint64_t)blockIdx.x * SB + threadIdx.x;
     const uint32_t N = (uint32_t)a.L.n_nodes;
     uint64_t cur[W];
+    if constexpr (!REPLAY && KIND == KIND_PREDICTOR_MIX && SB == 1024) {
+        // The image's granule (one per thread) is loaded first, then both envs of the pair
+        // (unconditional loads, clamped addresses, so the granule's wait counts only itself:
+        // vmcnt(4)); the granule is written and the barrier passed while the state is in flight,
+        // and the draws follow the barrier. Staged after the draws instead, the barrier waited
+        // for every wave's Philox burst and the state loads: 9.21 -> 8.98 us per launch at 1M envs
+        // (profiles/r02_step_stage_first_ab.txt; phase stamps r02_step_stamps.json)
+        const Thr32 X = thr32_layout(a.L);
+        const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.img) + a.L.bytes);
+        const uint32_t n16 = X.bytes / 16;
+        uint4 g = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x < n16) g = src[threadIdx.x];
+        uint64_t nx[W];
+        const uint64_t ec = e < a.B ? e : 0, en = e + stride < a.B ? e + stride : 0;
+        load_state<W>(a.state + ec * W, cur);
+        load_state<W>(a.state + en * W, nx);
+        if (threadIdx.x < n16) reinterpret_cast<uint4*>(lds)[threadIdx.x] = g;
+        for (uint32_t k = threadIdx.x + SB; k < n16; k += SB) reinterpret_cast<uint4*>(lds)[k] = src[k];
+        __syncthreads();
+        k_step_single<W, KIND, STORE, SB, true>(a, lds, e, stride, cur, N, &nx);
+        return;
+    }
     if (e < a.B) load_state<W>(a.state + e * W, cur);
     if constexpr (!REPLAY) {
         // Step mode: the draws depend on (seed, update counter, env id) only, so every
@@ -1349,6 +1415,18 @@ int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, in
     void* kargs[] = {&c};
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3((unsigned)sb), kargs, lds, (hipStream_t)stream);
 }
+
+#ifdef PBN_STAMPS
+}  // namespace pbn
+extern "C" int pbn_exp_stamps(void* out, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pbn::g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int pbn_exp_stamps_clear() {
+    static uint64_t z[16384 * 8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(pbn::g_stamps), z, sizeof z, 0, hipMemcpyHostToDevice);
+}
+namespace pbn {
+#endif
 
 // Advances the device-side update counter by k at the end of a captured run of step launches.
 __global__ void k_bump(uint64_t* p, uint64_t k) {
