@@ -319,6 +319,26 @@ def test_full_size_shard_invariance_and_sampled_oracle(G, oracle_mod):
     assert not (got[:, 3] >> np.uint64(199 - 192)).any()
 
 
+@pytest.mark.parametrize("B,base", [(1_000_003, 77), (1_000_001, 64)])
+def test_large_ragged_batch_step_matches_oracle(G, oracle_mod, B, base):
+    """The 1024-thread step path (image staged ahead of the state loads, clamped loads for lanes
+    past B) on ragged batches of ~1M envs with an odd env base (one Philox call per env) and an even
+    one (paired calls): sampled envs, the first and the last ones, equal the oracle after T steps."""
+    T = 3
+    net = load_network("bittner199")
+    b = G.PBNBatch(net, B, seed=4242, env_id_base=base)
+    b.randomize()
+    init = b.get_state()
+    b.step(T)
+    got = b.get_state()
+    b.close()
+    idx = np.concatenate([np.arange(4), np.arange(B - 4, B), np.random.default_rng(3).choice(B, 300, replace=False)])
+    o = oracle_mod.Oracle(net)
+    for e in idx:
+        assert np.array_equal(o.step_philox(init[e:e + 1], 4242, base + int(e), 0, T)[0], got[e]), e
+    assert not (got[:, 3] >> np.uint64(199 - 192)).any()
+
+
 def test_max_batch_single_gpu_sampled_oracle(G, oracle_mod):
     """BASELINE config 4's whole batch (8,388,608 envs, 256 MiB of state) on one GPU: step and
     rollout equal the oracle on sampled envs across the id range, bits past node 198 stay clear."""
