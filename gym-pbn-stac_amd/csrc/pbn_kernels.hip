@@ -85,6 +85,10 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
 #pragma unroll
         for (int k = 0; k < W; ++k) nxt[k] = (*pre_nxt)[k];
         draws(e);
+#ifdef PBN_STAMPS
+        st[2] = st[0];  // the caller's barrier was passed on entry here
+        st[1] = __builtin_amdgcn_s_memrealtime();
+#endif
     } else {
     if (e + po < a.B) load_state<W>(a.state + (e + po) * W, nxt);
     draws(e);
@@ -115,6 +119,40 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             st[3] = __builtin_amdgcn_s_memrealtime();
         }
 #endif
+        if constexpr (STORE == STORE_DIRTY) {
+            // Both envs evaluated first (plane writes and reads of env 1 issued right behind env 0's;
+            // LDS runs a wave's operations in order, so reusing the column needs no wait), then both
+            // stores: with env 0's store issued before env 1's loads were consumed, the compiler
+            // waited for that store to complete (vmcnt(0)) before env 1's plane writes.
+            // Env 1 is evaluated unconditionally (past B: junk from a clamped or skipped load,
+            // never stored).
+            auto eval = [&](const uint64_t (&s)[W], uint32_t i, uint64_t r, uint64_t q, uint32_t& self) {
+                to_plane<W>(P, s);
+                self = P.get(i >> 5);
+                if constexpr (KIND == KIND_PREDICTOR_MIX)
+                    return predictor_apply(P, i, self, r);
+                else
+                    return table_eval_lds(P, i, q, lds, a.L);
+            };
+            uint32_t self0, self1;
+            const uint32_t y0 = eval(cur, i0, r0, q0, self0);
+            const uint32_t y1 = eval(nxt, i1, r1, q1, self1);
+            // store the whole env (32 B at W = 4), and only if its bit changed: a full aligned env
+            // write measured faster than writing just the 16-B half that holds node i (7.69 vs
+            // 7.93 us at 1M envs), partial sector writes cost extra. The env's words are still in
+            // registers: bit i is flipped there (one 64-bit select per word) rather than written to
+            // the plane and all 2W dwords read back
+            auto put = [&](const uint64_t (&s)[W], uint64_t eh, uint32_t i) {
+                uint64_t out[W];
+                const uint32_t wi = i >> 6;
+                const uint64_t m = 1ull << (i & 63u);
+#pragma unroll
+                for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
+                store_state<W>(a.state + eh * W, out);
+            };
+            if (((self0 >> (i0 & 31u)) & 1u) != y0) put(cur, e, i0);
+            if (e1 < a.B && ((self1 >> (i1 & 31u)) & 1u) != y1) put(nxt, e1, i1);
+        } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint64_t eh = h ? e1 : e;
@@ -130,26 +168,11 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             else
                 y = table_eval_lds(P, i, h ? q1 : q0, lds, a.L);
             const uint32_t nv = (self & ~(1u << sh)) | (y << sh);
-            if constexpr (STORE == STORE_DIRTY) {
-                // store the whole env (32 B at W = 4), and only if its bit changed: a full
-                // aligned env write measured faster than writing just the 16-B half that holds
-                // node i (7.69 vs 7.93 us at 1M envs), partial sector writes cost extra
-                if (nv != self) {
-                    // the env's words are still in registers: flip bit i there (one 64-bit select
-                    // per word) rather than writing the plane and reading all 2W dwords back
-                    uint64_t out[W];
-                    const uint32_t wi = i >> 6;
-                    const uint64_t m = 1ull << (i & 63u);
-#pragma unroll
-                    for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
-                    store_state<W>(a.state + eh * W, out);
-                }
-            } else {
-                P.put(d, nv);
-                uint64_t out[W];
-                from_plane<W>(P, out);
-                store_state<W>(a.state + eh * W, out);
-            }
+            P.put(d, nv);
+            uint64_t out[W];
+            from_plane<W>(P, out);
+            store_state<W>(a.state + eh * W, out);
+        }
         }
 #ifdef PBN_STAMPS
         if (!st[4]) st[4] = __builtin_amdgcn_s_memrealtime();  // the first pair's stores issued
