@@ -533,7 +533,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         // records in rows of rs, slot tp4 holding the record a = 2^32 - 1 selects. Staged once
         // per persistent workgroup, so this computes the conversion instead of reading the
         // compact image (the env config's image does not carry it)
-        const uint64_t* gthr = reinterpret_cast<const uint64_t*>(a.img);
+        const uint64_t* gthr = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(a.img) + a.L.off_thr);
         const uint32_t tp = a.L.tp, tp4 = X.tp4, rs = X.rs;
         for (uint32_t k = threadIdx.x; k < N * tp4; k += BLOCK) {
             const uint32_t i = k / tp4, q = k - i * tp4;
