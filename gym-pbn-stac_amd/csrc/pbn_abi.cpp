@@ -179,6 +179,7 @@ struct pbn_batch {
     hipGraphExec_t step_graph[STEP_GRAPH_SIZES] = {};
     bool step_graph_built = false;
     bool step_graph_broken = false;       // capture or instantiation failed once: plain launches
+    bool exact_broken = false;            // an exact-length capture failed once: no more of them
     // exact-length graphs: one replay for a whole call of n steps (pbn_step_prepare, or the second
     // call with the same n); each extra replay in a call costs a graph start on the device (~13 us)
     static constexpr int EXACT_GRAPHS = 4;
@@ -280,13 +281,14 @@ static int build_predictor_image(const pbn_net_desc* d, pbn_net* n) {
     L.off_thr = 0;
     L.off_rec = align16(8u * L.tp * (uint32_t)N);
     L.bytes = align16(L.off_rec + 8u * pmax * (uint32_t)N);
-    {  // the Philox kernels' compact LDS image (thr32_layout, pbn_device.hpp) fits the same budget
+    {  // the Philox kernels' compact LDS image (thr32_layout, pbn_device.hpp): their planes follow it
         const uint32_t tp4 = (L.tp + 3u) & ~3u, rs = std::max(tp4 + 1u, pmax);
-        L.bytes = std::max(L.bytes, align16(align16(4u * tp4 * (uint32_t)N) + 8u * rs * (uint32_t)N));
+        L.plane_off = std::max(L.bytes, align16(align16(4u * tp4 * (uint32_t)N) + 8u * rs * (uint32_t)N));
     }
     L.kind = KIND_PREDICTOR_MIX;
     L.n_nodes = N;
-    if (L.bytes > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "network tables (%u B) exceed the LDS budget", L.bytes);
+    if (L.plane_off > MAX_IMAGE)
+        return fail(PBN_E_UNSUPPORTED, "network tables (%u B) exceed the LDS budget", L.plane_off);
     n->image.assign(L.bytes, 0);
     uint8_t* im = n->image.data();
     for (int i = 0; i < N; i++) {
@@ -367,6 +369,7 @@ static int build_table_image(const pbn_net_desc* d, pbn_net* n) {
     if (total > MAX_IMAGE) return fail(PBN_E_UNSUPPORTED, "probability tables (%llu B) exceed the LDS budget",
                                        (unsigned long long)total);
     L.bytes = align16((uint32_t)total);
+    L.plane_off = L.bytes;
     L.kind = KIND_PROB_TABLE;
     L.n_nodes = N;
     n->image.assign(L.bytes, 0);
@@ -541,9 +544,9 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (!b->d_image) return bail(fail(PBN_E_NOMEM, "network image upload failed"));
     if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, BLOCK, &b->bpc_base)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
-    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, b->step_block, &b->bpc_step)))
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.plane_off, b->step_block, &b->bpc_step)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
-    if ((rc = max_blocks_step(b->W, net->kind, net->L.bytes, BLOCK, &b->bpc_roll, 1, b->roll_group)))
+    if ((rc = max_blocks_step(b->W, net->kind, net->L.plane_off, BLOCK, &b->bpc_roll, 1, b->roll_group)))
         return bail(fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)rc)));
     if (hipStreamSynchronize(b->stream) != hipSuccess) return bail(fail(PBN_E_HIP, "stream sync"));
     *out = b;
@@ -851,34 +854,45 @@ static bool step_graph_ready(pbn_batch* b) {
 // Captures n step launches as one graph in a free (or the least recently used) exact-length slot.
 // Returns the slot, or -1 (plain launches / power-of-two graphs then).
 static int exact_graph_build(pbn_batch* b, uint32_t n) {
-    if (n < 2 || n > STEP_GRAPH_K || b->step_graph_broken || b->step_graph_off || !b->stream) return -1;
+    if (n < 2 || n > STEP_GRAPH_K || b->step_graph_broken || b->step_graph_off || b->exact_broken || !b->stream)
+        return -1;
     if (b->s_ubase.ensure(64)) return -1;
-    int slot = 0;
-    for (int j = 1; j < pbn_batch::EXACT_GRAPHS; ++j)
-        if (b->exact_used[j] < b->exact_used[slot]) slot = j;
-    if (b->exact_graph[slot]) {
-        (void)hipGraphExecDestroy(b->exact_graph[slot]);
-        b->exact_graph[slot] = nullptr;
-        b->exact_n[slot] = 0;
-    }
+    // capture and instantiate into a fresh exec first: a failed capture leaves the cached graphs
+    // as they were and marks the batch, so later calls do not re-capture n launches to fail again
     // no k_bump: pbn_step writes the device counter before every replay of an exact graph
     hipGraph_t g = nullptr;
+    hipGraphExec_t x = nullptr;
     bool ok = hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
     bool launched = ok;
     for (uint32_t k = 0; launched && k < n; ++k)
         launched = step_launch(b, 1, k, 0, nullptr, nullptr, (const uint64_t*)b->s_ubase.p, false) == 0;
     if (ok) ok = hipStreamEndCapture(b->stream, &g) == hipSuccess && launched && g;
-    if (ok) ok = hipGraphInstantiate(&b->exact_graph[slot], g, nullptr, nullptr, 0) == hipSuccess;
+    if (ok) ok = hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess;
     // upload now, so the first replay (e.g. a timed one) does not pay for it
-    if (ok) ok = hipGraphUpload(b->exact_graph[slot], b->stream) == hipSuccess;
+    if (ok) ok = hipGraphUpload(x, b->stream) == hipSuccess;
     if (g) (void)hipGraphDestroy(g);
     if (!ok) {
-        if (b->exact_graph[slot]) (void)hipGraphExecDestroy(b->exact_graph[slot]);
-        b->exact_graph[slot] = nullptr;
+        if (x) (void)hipGraphExecDestroy(x);
+        b->exact_broken = true;
         (void)hipGetLastError();
         g_err.clear();
         return -1;
     }
+    int slot = 0;
+    for (int j = 1; j < pbn_batch::EXACT_GRAPHS; ++j)
+        if (b->exact_used[j] < b->exact_used[slot]) slot = j;
+    if (b->exact_graph[slot]) {
+        // the evicted exec may still be queued or running from an earlier asynchronous pbn_step on
+        // this stream (HIP documents no deferred free): drain the stream first. Eviction happens
+        // only at capture time, never in a steady replay loop.
+        if (hipStreamSynchronize(b->stream) != hipSuccess) {
+            (void)hipGraphExecDestroy(x);
+            (void)fail(PBN_E_HIP, "stream sync before graph eviction failed");
+            return -1;
+        }
+        (void)hipGraphExecDestroy(b->exact_graph[slot]);
+    }
+    b->exact_graph[slot] = x;
     b->exact_n[slot] = n;
     b->exact_used[slot] = ++b->exact_clock;
     return slot;
@@ -1230,6 +1244,7 @@ int pbn_envcfg_create(const pbn_net* net, const pbn_envcfg_desc* d, pbn_envcfg**
         nd[2 * i + 1] = plus[1] - minus[1];
     }
     c->L.bytes = bytes;
+    c->L.plane_off = bytes;
     c->reset_care.assign(d->reset_care, d->reset_care + (size_t)c->H_reset * W);
     c->reset_value.assign(d->reset_value, d->reset_value + (size_t)c->H_reset * W);
     c->horizon = d->horizon;
@@ -1344,7 +1359,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         }
     }
     int bpc = 1;
-    if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc))
+    if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc, b->net->N))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
     if (b->env_bpc) bpc = std::min(bpc, b->env_bpc);
     EnvArgs a{};

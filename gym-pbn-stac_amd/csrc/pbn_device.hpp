@@ -238,9 +238,11 @@ __device__ __forceinline__ uint64_t predictor_record(uint32_t i, uint64_t k53, c
 // passes. Thresholds are non-decreasing, so the never-entries of a node are its last tp - m_i;
 // record slots q >= m_i all hold record m_i (slot rs >= tp4 + 1 per node), and the count's
 // overshoot at a = 2^32 - 1 lands on the same record. Bit-exact with predictor_record(i, u32_k53(a)).
-// Layout: thr32 [N][tp4] at 0, records u64 [N][rs] at rec_off (16-aligned); never larger than
-// the u64 image's L.bytes (the host pads L.bytes to cover it). The host builds it
-// (build_predictor_image, pbn_abi.cpp) and appends it to the device image at offset L.bytes.
+// Layout: thr32 [N][tp4] at 0, records u64 [N][rs] at rec_off (16-aligned). For pmax <= 3 it is
+// larger than the u64 image, so the kernels that stage it place their planes at L.plane_off =
+// max(L.bytes, its size); L.bytes itself stays the u64 image's size (what every other kernel and
+// the env config stage). The host builds it (build_predictor_image, pbn_abi.cpp) and appends it
+// to the device image at offset L.bytes.
 struct Thr32 {
     uint32_t tp4, rs, rec_off, bytes;
 };
@@ -306,9 +308,10 @@ __device__ __forceinline__ uint32_t table_eval_lds(const P_t& P, uint32_t i, uin
 
 // Env record (k_env, cooperative-draw mode): predictor record rec (in0 | in1<<16 | in2<<32 | tt<<48)
 // of node i re-encoded for the LDS state planes of 256-lane workgroups: byte offsets of the plane
-// dwords holding in0 / in1 (x), in2 / node i (y), the bit positions in those dwords (z, one byte
-// each: in0, in1, in2, i), tt | i << 16 (w). An update then reads its four plane dwords with no
-// index arithmetic. Inputs are < 512 (W <= 8), so every offset is < 16 KiB.
+// dwords holding in0 / in1 (x), in2 / node i (y), tt | i << 16
+// (w): the bit positions of in0, in1, in2, i in those dwords (one byte each). An update then reads
+// its four plane dwords with no index arithmetic. Inputs are < 512 (W <= 8), so every offset is
+// < 16 KiB.
 __device__ __forceinline__ uint4 env_record(uint64_t rec, uint32_t i) {
     const uint32_t x0 = (uint32_t)rec & 0xFFFFu, x1 = (uint32_t)(rec >> 16) & 0xFFFFu,
                    x2 = (uint32_t)(rec >> 32) & 0xFFFFu;

@@ -26,6 +26,9 @@ namespace pbn {
 // Measurement builds only (tools/build_exp.sh -DPBN_STAMPS): per-wave s_memrealtime stamps (100 MHz)
 // of the step kernel's phases, kept in registers and written once at the end of the wave.
 __device__ uint64_t g_stamps[16384 * 8];
+// k_env (cooperative-draw path): per wave, ENV_STAMPS words (tools/env_stamps.py reads them)
+constexpr int ENV_STAMPS = 16;
+__device__ uint64_t g_env_stamps[16384 * ENV_STAMPS];
 #endif
 
 // ------------------------------------------------------------------ step
@@ -105,7 +108,7 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
 #ifdef PBN_STAMPS
     st[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.plane_off) + threadIdx.x};
     while (e < a.B) {
         const uint64_t e1 = e + po;
         uint64_t r0 = 0, r1 = 0;
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(SB) void k_rollout(StepArgs a) {
     else
         stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
-    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.plane_off) + threadIdx.x};
     // Envs 2m / 2m + 1 share their Philox calls (pbn_device.hpp). With an even env base the lane
     // pair holds such a pair, and for updates t, t + 1 the even lane computes the call of t, the
     // odd lane that of t + 1, and they swap the two words the other needs: one call per lane
@@ -514,6 +517,7 @@ struct RankMagic {
 };
 __constant__ constexpr RankMagic kRankMagic{};
 
+
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     constexpr bool GEN = FAST == 2 || FAST == 4;
@@ -559,6 +563,16 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     }
     __syncthreads();
     const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes + a.erec_shift) + threadIdx.x};
+#ifdef PBN_STAMPS
+    // 0 start, 1 first chunk below ENV_OWN_DRAWS_MIN active lanes, 2 first chunk after a lane of the
+    // wave found the work queue empty,
+    // 3/4/5/6 first chunk with <= 32 / 16 / 8 / 2 active lanes, 7 end; 8 chunks, 9 sum of active
+    // lanes over chunks, 10 chunks in the tail (queue empty), 11 sum of active lanes there,
+    // 12 block, 13 hw id, 14 env steps of the wave that hit the update cap
+    uint64_t est[ENV_STAMPS] = {};
+    uint32_t ncapped = 0;
+    est[0] = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
     const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
     const uint2* ndelta = reinterpret_cast<const uint2*>(lds + a.off_ndelta);
@@ -649,6 +663,25 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             if (__ballot(!exhausted) == 0) break;
             continue;
         }
+#ifdef PBN_STAMPS
+        if constexpr (GEN) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            const uint32_t na = (uint32_t)__popcll(act);
+            const bool qe = __ballot(exhausted) != 0;  // a lane of this wave found the queue empty
+            if (!est[1] && na < ENV_OWN_DRAWS_MIN) est[1] = now;
+            if (!est[2] && qe) est[2] = now;
+            if (!est[3] && na <= 32) est[3] = now;
+            if (!est[4] && na <= 16) est[4] = now;
+            if (!est[5] && na <= 8) est[5] = now;
+            if (!est[6] && na <= 2) est[6] = now;
+            est[8] += 1;
+            est[9] += na;
+            if (qe) {
+                est[10] += 1;
+                est[11] += na;
+            }
+        }
+#endif
         uint16_t* gbuf = nullptr;
         if constexpr (GEN) {
             // ---- cooperative draw generation for the next ENV_CHUNK updates of every active lane
@@ -792,7 +825,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                                    (__builtin_amdgcn_ubfe(b2, q.z >> 16, 1) << 1) | xs;
                 const uint32_t y = __builtin_amdgcn_ubfe(q.w, p, 1);
                 const uint32_t fl = (xs ^ y) & (act ? 1u : 0u);  // the bit changes (and is applied)
-                *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(pb) + (q.y >> 16)) = self ^ (fl << shs);
+                *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(pb) + (q.y >> 16)) = self ^ (fl << (shs & 31u));
                 used += act ? 1u : 0u;
                 pfl = fl;
                 psg = y - 1u;  // 0 (y = 1) or all ones (y = 0)
@@ -801,6 +834,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             if (__ballot(act) == 0) break;
             }
             };
+
             if (__ballot(lim < ENV_CHUNK) != 0)
                 chunk(std::true_type{});
             else
@@ -872,9 +906,21 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
         a.reward[eo] = (term ? a.reward_success : 0) - a.action_cost * n_act;  // :218-222
         a.flags[eo] = (uint8_t)((term ? 1 : 0) | (nst == a.horizon ? 2 : 0) | (capped ? 4 : 0));
         a.n_updates[eo] = used;
+#ifdef PBN_STAMPS
+        ncapped += capped ? 1u : 0u;
+#endif
         ++t;
         begin_steps(s);
     }
+#ifdef PBN_STAMPS
+    est[7] = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t k = 0; k < 64; ++k) est[14] += (uint32_t)__shfl((int)ncapped, (int)k);
+    est[12] = blockIdx.x;
+    est[13] = __smid();
+    const uint32_t wv = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    if (lane == 0 && wv < 16384)
+        for (int k = 0; k < ENV_STAMPS; ++k) g_env_stamps[(uint64_t)wv * ENV_STAMPS + k] = est[k];
+#endif
 }
 
 // ------------------------------------------------------------------ R6, group mode
@@ -1247,7 +1293,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout_grp(StepArgs a) {
     const uint32_t k = lane & (G - 1);
     const uint32_t gbase = lane & ~(uint32_t)(G - 1);
     const uint32_t gmask = (1u << G) - 1u;
-    uint32_t* row = reinterpret_cast<uint32_t*>(lds + a.L.bytes) + (threadIdx.x / G) * (2 * W);
+    uint32_t* row = reinterpret_cast<uint32_t*>(lds + a.L.plane_off) + (threadIdx.x / G) * (2 * W);
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1429,7 +1475,7 @@ int launch_step(int W, const StepArgs& a, int store_mode, int replay, int sb, in
     if (grp > 1) sb = BLOCK;
     void* fn = step_kernel(W, a.L.kind, store_mode, replay, sb, rollout, grp);
     if (!fn) return (int)hipErrorInvalidValue;
-    const uint32_t lds = step_lds_bytes(W, a.L.bytes, sb, grp);
+    const uint32_t lds = step_lds_bytes(W, replay ? a.L.bytes : a.L.plane_off, sb, grp);
     if (lds > 64u * 1024u) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
@@ -1445,8 +1491,13 @@ extern "C" int pbn_exp_stamps(void* out, size_t bytes) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pbn::g_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 extern "C" int pbn_exp_stamps_clear() {
-    static uint64_t z[16384 * 8];
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(pbn::g_stamps), z, sizeof z, 0, hipMemcpyHostToDevice);
+    static uint64_t z[16384 * pbn::ENV_STAMPS];
+    int rc = (int)hipMemcpyToSymbol(HIP_SYMBOL(pbn::g_stamps), z, 16384 * 8 * 8, 0, hipMemcpyHostToDevice);
+    if (!rc) rc = (int)hipMemcpyToSymbol(HIP_SYMBOL(pbn::g_env_stamps), z, sizeof z, 0, hipMemcpyHostToDevice);
+    return rc;
+}
+extern "C" int pbn_exp_env_stamps(void* out, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pbn::g_env_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 namespace pbn {
 #endif
@@ -1501,7 +1552,8 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, replay, a.fast, a.grp)
                                               : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast, a.grp);
     EnvArgs c = a;
-    return launch(fn, grid, env_lds_bytes(W, a.L.bytes + a.erec_shift, replay ? std::min(a.fast, 1) : a.fast, a.grp),
+    return launch(fn, grid, env_lds_bytes(W, a.L.bytes + a.erec_shift, replay ? std::min(a.fast, 1) : a.fast, a.grp,
+                                          a.L.n_nodes),
                   stream, &c, sizeof c);
 }
 
@@ -1524,16 +1576,17 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb, grp), blocks_per_cu);
 }
 
-uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp) {
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes) {
     if (fast == 3) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
     const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
+    (void)n_nodes;
     return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES : planes;
 }
 
-int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu) {
+int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes) {
     void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast, grp)
                                           : env_fn_w<KIND_PROB_TABLE>(W, 0, fast, grp);
-    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast, grp), blocks_per_cu);
+    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast, grp, n_nodes), blocks_per_cu);
 }
 
 }  // namespace pbn

@@ -36,6 +36,10 @@ struct NetLayout {
     int32_t n_nodes;
     uint32_t tp;        // predictor mix: thresholds per node (even)
     uint32_t pmax;      // predictor mix: record slots per node
+    // LDS offset of the state planes of k_step / k_rollout / k_rollout_grp: max(bytes, the compact
+    // image's size) for predictor mix (those kernels stage the compact image, which for pmax <= 3
+    // is larger than the u64 one), bytes for tables. Every other kernel places its planes at bytes.
+    uint32_t plane_off;
 };
 
 struct StepArgs {
@@ -181,8 +185,9 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_unpack(const uint64_t* words, uint8_t* out, uint64_t B, uint32_t N, uint32_t W, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout = 0, int grp = 1);
-int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu);
-uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp);
+int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes = 0);
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes = 0);
+
 #ifndef PBN_ENV_CHUNK
 #define PBN_ENV_CHUNK 32
 #endif

@@ -78,13 +78,14 @@ def _pbn_target(graph=None, goal_config=None, render_mode=None, render_no_cache=
     reward_config = envs.PBNEnv._check_config(
         reward_config, "reward", {"successful_reward", "wrong_attractor_cost", "action_cost"},
         default_values={"successful_reward": 10, "wrong_attractor_cost": 2, "action_cost": 1})
+    # subscripts, as pbn_target.py:61-64: with exactly one key missing _check_config passes and
+    # the subscript raises KeyError
+    goal = (goal_config["target_nodes"], goal_config["target_node_values"],
+            goal_config["undesired_node_values"], goal_config["intervene_on"])
     if all_attractors is None:
         raise ValueError("all_attractors is required (cabean output; see gym_pbn_amd.io.cabean)")
     env = envs.PBNTargetEnv(graph, all_attractors, horizon=goal_config.get("horizon", 100), name=name, **kw)
-    env.target_nodes = goal_config.get("target_nodes")
-    env.target_node_values = goal_config.get("target_node_values")
-    env.undesired_node_values = goal_config.get("undesired_node_values")
-    env.intervene_on = goal_config.get("intervene_on")
+    env.target_nodes, env.target_node_values, env.undesired_node_values, env.intervene_on = goal
     env.successful_reward = reward_config["successful_reward"]
     env.wrong_attractor_cost = reward_config["wrong_attractor_cost"]
     env.action_cost = reward_config["action_cost"]

@@ -169,6 +169,100 @@ def test_exact_length_step_graphs_match_oracle(G, oracle_mod):
     b.close()
 
 
+def test_config2_exact_size_matches_oracle(G, oracle_mod):
+    """BASELINE config 2 at its exact size: 65,536 Bittner-28 envs (Graph.step, base.py:306-312).
+    The library's own choices at this size, no overrides: step runs of 20 launches go out as one
+    graph replay, and rollout picks the 2-lanes-per-env group kernel (k_rollout_grp<1,2>). Every env
+    against the oracle."""
+    net = load_network("bittner28")
+    o = oracle_mod.Oracle(net)
+    B, seed = 65536, 0x5EED
+    b = G.PBNBatch(net, B, seed=seed)
+    b.randomize()
+    init = b.get_state()
+    assert np.array_equal(init, o.init_philox(B, seed=seed))
+    b.step(20)
+    b.step(20)  # the second call of the same length replays its captured graph
+    assert np.array_equal(b.get_state(), o.step_philox(init, seed, 0, 0, 40, n_threads=8))
+    b.rollout(256)
+    assert b.info()["roll_lanes"] == 2
+    assert np.array_equal(b.get_state(), o.step_philox(init, seed, 0, 0, 40 + 256, n_threads=8))
+    b.close()
+
+
+def test_exact_graph_eviction_without_host_sync(G, oracle_mod):
+    """Six lengths cycled through the four exact-length slots with no host sync between calls: every
+    capture past the fourth evicts a graph whose replay may still be queued on the batch stream
+    (pbn_abi.cpp exact_graph_build drains the stream before destroying it). The state after the
+    whole run equals the oracle's."""
+    net = load_network("bittner199")
+    o = oracle_mod.Oracle(net)
+    b = G.PBNBatch(net, 20001, seed=23, env_id_base=2)
+    b.randomize()
+    init = b.get_state()
+    done = 0
+    for _ in range(2):
+        for n in (4, 6, 9, 12, 17, 25):  # each length twice in a row: captured at its second call
+            b.step(n)
+            b.step(n)
+            done += 2 * n
+    assert np.array_equal(b.get_state(), o.step_philox(init, 23, 2, 0, done))
+    b.close()
+
+
+def _syn_cubes(rng, n_nodes, n_cubes, n_care):
+    """Random attractor cubes over n_care nodes each (attractor h = cube h), packed [H][W]."""
+    W = (n_nodes + 63) // 64
+    care = np.zeros((n_cubes, W), np.uint64)
+    value = np.zeros((n_cubes, W), np.uint64)
+    for h in range(n_cubes):
+        for i in rng.choice(n_nodes, n_care, replace=False):
+            care[h, i // 64] |= np.uint64(1) << np.uint64(i % 64)
+            if rng.random() < 0.5:
+                value[h, i // 64] |= np.uint64(1) << np.uint64(i % 64)
+    return care, value
+
+
+@pytest.mark.parametrize("n_nodes", [150, 500])
+def test_small_pmax_network_matches_oracle(G, oracle_mod, n_nodes):
+    """pmax = 2 (every node two predictors): the compact image of the Philox kernels is larger than
+    the u64 image here, so k_step / k_rollout place their planes past it (NetLayout.plane_off) while
+    the env kernel stages the u64 image's size. Step, rollout and the R6 env step vs the oracle."""
+    from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
+
+    net = PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(n_nodes, 2, seed=n_nodes, ragged=False),
+                                               name=f"syn{n_nodes}p2")
+    o = oracle_mod.Oracle(net)
+    B, seed, base = 6000, 31, 4
+    b = G.PBNBatch(net, B, seed=seed, env_id_base=base)
+    b.randomize()
+    init = b.get_state()
+    b.step(5)
+    b.rollout(7)
+    assert np.array_equal(b.get_state(), o.step_philox(init, seed, base, 0, 12))
+    # R6: three cubes over 5 nodes each; attractor 0 for reset, the last as target
+    care, value = _syn_cubes(np.random.default_rng(n_nodes), n_nodes, 3, 5)
+    gnet = G.Net(net)
+    cfg = G.EnvConfig(gnet, G.attractors_from_cubes(care, value, np.arange(3), n_nodes), horizon=10)
+    cfgd = dict(care=care, value=value, target_care=care[2], target_value=value[2], reset_care=care[:1],
+                reset_value=value[:1], horizon=10)
+    e = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
+    e.env_reset(cfg)
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), care[:1], value[:1],
+                                seed=seed, env_base=base, reset_count=0)
+    assert np.array_equal(e.get_state(), st)
+    rng = np.random.default_rng(1)
+    for t in range(3):
+        acts = rng.integers(0, n_nodes + 1, size=(B, 2)).astype(np.int32)
+        obs, rew, flags, nup = e.env_step_multi(cfg, acts, update_cap=2048)
+        ref = o.env_step_multi(cfgd, st, ns, acts, seed=seed, env_base=base, call_idx=t, update_cap=2048)
+        assert np.array_equal(nup, ref["n_updates"]) and np.array_equal(obs, ref["obs"]), t
+        assert np.array_equal(rew, ref["reward"]) and np.array_equal(flags, ref["flags"]), t
+        st, ns = ref["state"], ref["n_steps"]
+    b.close()
+    e.close()
+
+
 def test_step_inside_a_torch_graph_capture(G, oracle_mod):
     """pbn_step on a stream the caller is capturing (torch.cuda.graph) launches plainly into the
     caller's graph instead of capturing one of its own; replaying the caller's graph repeats the
@@ -623,10 +717,12 @@ def _random_cubes(rng, N, H, n_care):
                                   "b199_nogen", "tt200_fast", "syn500_gen",
                                   "syn300_wide_cube", "b28_first_tested", "b28_h12_first_tested",
                                   "tt200_first_tested", "b199_grp2", "b199_grp4", "b199_grp8", "b28_grp4_cap",
-                                  "b28_grp8_first_tested", "b28_grp2_h8", "b199_grp4_long"])
+                                  "b28_grp8_first_tested", "b28_grp2_h8", "b199_grp4_long",
+                                  "b28_gen_cap41", "b199_gen_long", "b199_gen_long_first_tested"])
 def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     """Every k_env variant (cooperative draw generation, byte counters without it, general
-    cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs."""
+    cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs and
+    long until-attractor loops (thousands of updates per env step, odd caps)."""
     from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
 
     rng = np.random.default_rng(zlib.crc32(case.encode()))
@@ -634,7 +730,7 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     first = case.endswith("first_tested")  # PBNTargetEnv.step(force=False) semantics
     # k_env_grp (G lanes per env, blocks of G updates resolved in parallel) or lane mode (1)
     monkeypatch.setenv("PBNSIM_ENV_GROUP", case.split("_grp")[1][0] if "_grp" in case else "1")
-    if case.startswith("b199_grp"):
+    if case.startswith("b199_grp") or case.startswith("b199_gen_long"):
         net = load_network("bittner199")
     elif case.startswith("b28"):
         net = load_network("bittner28")
@@ -649,9 +745,12 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
         n = 500 if case == "syn500_gen" else 300
         net = PredictorNetwork.from_predictor_sets(*synthetic_predictor_sets(n, 4, seed=n), name=f"syn{n}")
     N = net.n_nodes
-    if case in ("b28_gen_cap", "b28_grp4_cap"):
-        cap = 41 if "grp" in case else 40  # not a multiple of the group size
+    if case in ("b28_gen_cap", "b28_grp4_cap", "b28_gen_cap41"):
+        cap = 41 if ("grp" in case or "cap41" in case) else 40  # not a multiple of the group size
         attractors = [_random_cubes(rng, N, 2, 5), _random_cubes(rng, N, 2, 5)]
+    elif case.startswith("b199_gen_long"):  # long loops: thousands of updates per env step
+        cap = 2001
+        attractors = [_random_cubes(rng, N, 2, 12), _random_cubes(rng, N, 2, 4)]
     elif case == "b199_grp4_long":  # long until-attractor loops, many capped envs
         cap = 2001
         attractors = [_random_cubes(rng, N, 4, 12), _random_cubes(rng, N, 2, 4)]
@@ -686,11 +785,11 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
         assert np.array_equal(b.get_state(), st), case
         if "_grp" in case:
             assert b.info()["env_lanes"] == int(case.split("_grp")[1][0])  # group mode really ran
-        if case in ("b28_gen_cap", "b28_first_tested"):
+        if case in ("b28_gen_cap", "b28_first_tested", "b28_gen_cap41") or case.startswith("b199_gen_long"):
             assert b.info()["env_kernel"] == 4  # wave-generated draws, one counter word (<= 4 cubes)
         if case in ("b28_h8_gen", "b199_h6_gen_first_tested"):
             assert b.info()["env_kernel"] == 2  # wave-generated draws, two counter words
-    if case in ("b28_gen_cap", "b28_grp4_cap", "b199_grp4_long"):
+    if case in ("b28_gen_cap", "b28_grp4_cap", "b199_grp4_long", "b28_gen_cap41") or case.startswith("b199_gen_long"):
         assert (flags & 4).any() and not (flags & 4).all()  # some envs capped, some reached an attractor
     assert (nup > 1).any()
 

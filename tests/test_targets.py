@@ -45,6 +45,12 @@ def test_pbn_target_v0_reference_constructor_checks():
              all_attractors=_atts())
     with pytest.raises(ValueError, match="all_attractors"):
         make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config=goal)
+    # exactly one goal key missing: _check_config passes (it raises only for more than one,
+    # pbn_target.py:232) and the subscript at pbn_target.py:61-64 raises KeyError
+    for k in goal:
+        one_missing = {kk: v for kk, v in goal.items() if kk != k}
+        with pytest.raises(KeyError, match=k):
+            make("gym-PBN/PBN-target-v0", graph="bittner28", goal_config=one_missing, all_attractors=_atts())
 
 
 @pytest.mark.gpu
