@@ -460,19 +460,19 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
     return out
 
 
-R6_HIGH_CAP = 1 << 20  # far above the longest loop measured at config 5 (profiles/r03_r6_cap_sweep.json)
+R6_HIGH_CAP = 1 << 20  # the longest loop measured at config 5 ran 78,057 updates (profiles/r03_r6_cap_sweep.json)
 
 
 def r6_supplement(args, world, rank, device, dist, valu):
     """BASELINE config 5 beside the main line (r6_figure): the fixture's attractors with the 4,096
-    update cap (the headline figure, ``args.r6_chunks`` chunks), plus, one chunk each, the same with
-    a cap the loop essentially never reaches (comparable to the reference's unbounded loop,
-    pbn_target_multi.py:135-146) and SURVEY §8(d)'s attractor spec with the 4,096 cap."""
+    update cap (the headline figure, ``args.r6_chunks`` chunks), plus, one chunk each and with a cap
+    the loop never reached in measurement (so comparable to the reference's unbounded loop,
+    pbn_target_multi.py:135-146): the same attractors, and SURVEY §8(d)'s attractor spec."""
     out = {"metric": "R6 env-steps/s (whole node) incl. per-chunk trajectory all-gather",
            **r6_figure(args, world, rank, device, dist, valu, "fixture", 4096, args.r6_chunks)}
     if args.r6_variants:
         out["high_cap"] = guarded(r6_figure, args, world, rank, device, dist, valu, "fixture", R6_HIGH_CAP, 1)
-        out["spec_attractors"] = guarded(r6_figure, args, world, rank, device, dist, valu, "spec", 4096, 1)
+        out["spec_attractors"] = guarded(r6_figure, args, world, rank, device, dist, valu, "spec", R6_HIGH_CAP, 1)
     return out
 
 

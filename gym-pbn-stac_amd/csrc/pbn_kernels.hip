@@ -1,10 +1,12 @@
 // pbn_kernels.hip -- gfx950 kernels of the vectorised PBN simulator.
 //
-// Mapping: one lane = one env (state in VGPRs), one 256-thread workgroup stages
-// the network image (node info, 53-bit selection thresholds, predictor records
-// or probability thresholds) into LDS once, then walks envs in a grid-stride loop.
-// The grid is sized to what is resident (CUs x blocks/CU), so the LDS staging is
-// paid once per resident workgroup, not once per 256 envs.
+// Mapping: one lane owns one env at a time; its state words are loaded into VGPRs and, for the
+// node update, spread over the lane's column of LDS state planes. Each workgroup stages the
+// network image (thresholds, predictor records or probability tables) into LDS once. Step mode
+// (the bench kernel, k_step<.., 1024>): 1024-thread workgroups, two per CU, every thread owning
+// one pair of envs (e, e + grid stride) at 1M envs (more pairs per thread, grid-stride, above);
+// rollout / R6 / SSD kernels: 256-thread workgroups sized to what is resident, lanes refilled
+// from a work counter (R6) or walking envs in a grid-stride loop.
 //
 // Reference semantics implemented (file:line in the reference):
 //   k_step    Graph.step base.py:306-312 (+ Node.Predstep :89-119) and
@@ -129,8 +131,15 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
             // waited for that store to complete (vmcnt(0)) before env 1's plane writes.
             // Env 1 is evaluated unconditionally (past B: junk from a clamped or skipped load,
             // never stored).
+            // the plane's last dword holds nodes >= 64W - 32 only: it is written only if N reaches it
+            // (Bittner-200: 7 of the 8 dwords, one LDS write of eight saved per env)
+            const bool last_dw = N > 64u * W - 32u;
             auto eval = [&](const uint64_t (&s)[W], uint32_t i, uint64_t r, uint64_t q, uint32_t& self) {
-                to_plane<W>(P, s);
+#pragma unroll
+                for (int k = 0; k < W; ++k) {
+                    P.put(2 * k, (uint32_t)s[k]);
+                    if (k + 1 < W || last_dw) P.put(2 * k + 1, (uint32_t)(s[k] >> 32));
+                }
                 self = P.get(i >> 5);
                 if constexpr (KIND == KIND_PREDICTOR_MIX)
                     return predictor_apply(P, i, self, r);
@@ -517,11 +526,24 @@ struct RankMagic {
 };
 __constant__ constexpr RankMagic kRankMagic{};
 
+// Inclusive prefix sum over the wave's 64 lanes (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast15 / row_bcast31 carry the row totals; lanes without a source add 0).
+__device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
 
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     constexpr bool GEN = FAST == 2 || FAST == 4;
     constexpr bool ONE_WORD = FAST == 4;  // <= 4 cubes: the high counter word is never read
+    constexpr bool TAIL = FAST == 4;      // wave-wide tail mode (see below)
     static_assert(!GEN || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
     extern __shared__ __align__(16) uint8_t lds[];
     const uint32_t N = (uint32_t)a.L.n_nodes;
@@ -589,6 +611,12 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
     int64_t nst = 0, dpos = 0, dend = 0;
     int n_act = 0;
     bool capped = false;
+    bool tmode = false;  // TAIL: this wave resolves its remaining envs one at a time, 64 updates per block
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
 
     // Start env step t (or the first later step whose action row is valid) of lane env e from
     // state s: flips (:120-131), observation before the update (:133), plane, counters. With no
@@ -682,7 +710,115 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
             }
         }
 #endif
+        bool done = false;
+        bool in_tail = false;
+        if constexpr (TAIL) {
+            // ---- tail mode: once the work queue has run dry (some lane found it empty) and the wave
+            // holds at most a.tail_max envs, the whole wave works on ONE env at a time (the lowest
+            // active lane's), resolving 64 consecutive updates per block: lane k takes update used + k
+            // (its Philox draw, predictor record and operands are state-independent), finds the last
+            // earlier lane of the block that wrote each operand (per-node 64-bit writer masks in the
+            // wave's LDS scratch), and the block's outputs are the fixed point of y_k = tt_k(operands
+            // from their writers or the block-start state): a DAG, so iterating from the block-start
+            // values settles in at most depth + 1 rounds and a round that changes nothing is exact.
+            // Packed counter deltas are prefix-summed over the wave; the first update whose counters
+            // hit a cube (or update 0 on o0, :134) ends the env step; the last writer of each node in
+            // the committed prefix sets its bit in the env's plane column. Bit-exact with lane mode.
+            // A long until-attractor loop left alone (the reference's unbounded loop,
+            // pbn_target_multi.py:135-146, the per-step launch's last envs) then advances 64 updates
+            // per block round trip instead of one per update.
+            if (tmode || (__popcll(act) <= a.tail_max && __ballot(exhausted) != 0)) {
+                in_tail = true;
+                uint64_t* wm = reinterpret_cast<uint64_t*>(lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES);
+                if (!tmode) {
+                    for (uint32_t k = lane; k < N; k += 64) wm[k] = 0ull;
+                    wave_sync();
+                    tmode = true;
+                }
+                const uint32_t L = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+                uint32_t u = (uint32_t)__shfl((int)used, (int)L);
+                uint32_t m = (uint32_t)__shfl((int)m_lo, (int)L);
+                const uint32_t h0 = (uint32_t)__shfl(hit0 ? 1 : 0, (int)L);
+                const uint64_t gid = a.env_base + (uint64_t)__shfl((long long)e, (int)L);
+                const uint32_t c1 = a.call_idx + (uint32_t)__shfl((int)t, (int)L);
+                uint32_t* col = P.base + ((int32_t)L - (int32_t)lane);  // lane L's plane column
+                const uint8_t* colb = reinterpret_cast<const uint8_t*>(col);
+                const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
+                const uint32_t* ndl = reinterpret_cast<const uint32_t*>(ndelta);
+                const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;
+                auto last_writer = [&](uint64_t wmask) -> int32_t {
+                    const uint64_t w = wmask & below;
+                    return w ? 63 - (int32_t)__clzll((long long)w) : -1;
+                };
+                bool fin = false, hitf = false;
+                while (!fin) {
+                    const uint32_t U = u + lane;  // this lane's update (blocks start at even indices)
+                    uint32_t w4[4];
+                    philox_draw(a.seed, U >> 1, c1, gid, STREAM_ENV, w4);
+                    const uint32_t odd = U & 1u;
+                    const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
+                    const uint4 q = erec[__umul24(i, X.rs) + predictor_choice32(i, odd ? w4[3] : w4[1], lds, X.tp4)];
+                    constexpr uint32_t ROW = BLOCK * 4u;  // env_record's plane offsets: dword * ROW
+                    const uint32_t o0 = q.x & 0xFFFFu, o1 = q.x >> 16, o2 = q.y & 0xFFFFu, os = q.y >> 16;
+                    const uint32_t n0 = (o0 / ROW) * 32u | (q.z & 31u), n1 = (o1 / ROW) * 32u | ((q.z >> 8) & 31u),
+                                   n2 = (o2 / ROW) * 32u | ((q.z >> 16) & 31u), ss = (q.z >> 24) & 31u;
+                    // block-start values of the operands (in0, in1, in2, own bit)
+                    const uint32_t v0 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + o0), q.z, 1);
+                    const uint32_t v1 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + o1), q.z >> 8, 1);
+                    const uint32_t v2 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + o2), q.z >> 16, 1);
+                    const uint32_t v3 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + os), ss, 1);
+                    atomicOr(reinterpret_cast<unsigned long long*>(&wm[i]), 1ull << lane);
+                    wave_sync();
+                    const uint64_t w0 = wm[n0], w1 = wm[n1], w2 = wm[n2], wi = wm[i];
+                    wave_sync();
+                    wm[i] = 0ull;  // the table is all zero again after every block
+                    const int32_t r0 = last_writer(w0), r1 = last_writer(w1), r2 = last_writer(w2),
+                                  r3 = last_writer(wi);
+                    uint32_t x3 = v3;
+                    uint32_t y = __builtin_amdgcn_ubfe(q.w, (v0 << 3) | (v1 << 2) | (v2 << 1) | v3, 1);
+                    if (__ballot(r0 >= 0 || r1 >= 0 || r2 >= 0 || r3 >= 0) != 0) {
+                        for (;;) {
+                            const uint64_t Y = __ballot(y != 0u);
+                            auto pick = [&](int32_t r, uint32_t v) { return r >= 0 ? (uint32_t)(Y >> r) & 1u : v; };
+                            x3 = pick(r3, v3);
+                            const uint32_t yn = __builtin_amdgcn_ubfe(
+                                q.w, (pick(r0, v0) << 3) | (pick(r1, v1) << 2) | (pick(r2, v2) << 1) | x3, 1);
+                            if (__ballot(yn != y) == 0) break;
+                            y = yn;
+                        }
+                    }
+                    // packed counter deltas (+ d for 0 -> 1, - d for 1 -> 0), prefix over the block
+                    const uint32_t sg = y - 1u;
+                    const uint32_t mk = m + wave_inclusive_add((((y ^ x3) ? ndl[2u * i] : 0u) ^ sg) - sg);
+                    const bool valid = U < a.update_cap;
+                    const bool hk = (U == 0u && !a.first_tested) ? h0 != 0u : has_zero_byte(mk) != 0u;
+                    const uint64_t SM = __ballot(valid && hk), VM = __ballot(valid);
+                    const uint32_t nd = SM ? (uint32_t)__ffsll((unsigned long long)SM) : (uint32_t)__popcll(VM);
+                    const uint64_t within = nd >= 64u ? ~0ull : ((1ull << nd) - 1ull);
+                    // commit: the last writer of each node among the first nd updates, if it changed the bit
+                    if (lane < nd && (wi & ~upto & within) == 0ull && y != v3) {
+                        uint32_t* dw = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + os);
+                        if (y)
+                            atomicOr(dw, 1u << ss);
+                        else
+                            atomicAnd(dw, ~(1u << ss));
+                    }
+                    m = (uint32_t)__shfl((int)mk, (int)(nd - 1u));
+                    u += nd;
+                    hitf = SM != 0ull;
+                    fin = hitf || u >= a.update_cap;
+                    wave_sync();
+                }
+                if (lane == L) {
+                    used = u;
+                    m_lo = m;
+                    capped = !hitf;
+                    done = true;
+                }
+            }
+        }
         uint16_t* gbuf = nullptr;
+        if (!in_tail) {
         if constexpr (GEN) {
             // ---- cooperative draw generation for the next ENV_CHUNK updates of every active lane
             uint8_t* gw = lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES;
@@ -747,7 +883,6 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 
         // ---- up to ENV_CHUNK updates of this lane's env
         const uint64_t g = a.env_base + (uint64_t)e;
-        bool done = false;
         if constexpr (GEN) {
             const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
             const uint8_t* pb = reinterpret_cast<const uint8_t*>(P.base);  // this lane's plane column
@@ -892,6 +1027,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                 break;
             }
         }
+        }  // !in_tail
         if (!done) continue;
 
         // ---- finish: outputs of step() (:148-154) into step t's slot, then the env's next step

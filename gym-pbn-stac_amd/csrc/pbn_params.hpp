@@ -112,6 +112,8 @@ struct EnvArgs {
                               // [n_calls][B]...; step t draws with Philox c1 = call_idx + t
     uint32_t erec_shift;      // fast == 2: LDS bytes the 16-B env records add over the 8-B records
                               // (off_cubes / off_target / off_ndelta / off_gen are LDS offsets)
+    uint32_t tail_max;        // fast == 4: a wave whose queue ran dry resolves its envs one at a time,
+                              // 64 updates per block, once it holds at most this many (0 = never)
 };
 
 constexpr uint32_t MT_ROW = 624;
@@ -196,6 +198,9 @@ constexpr uint32_t ENV_CHUNK = PBN_ENV_CHUNK;  // updates per lane between refil
 #define PBN_ENV_UNROLL 8
 #endif
 constexpr uint32_t ENV_UNROLL = PBN_ENV_UNROLL;  // updates between the wave's "any lane active" tests
+// k_env tail mode: live envs per wave at (or below) which a wave whose queue ran dry switches to
+// resolving one env at a time across all 64 lanes (PBNSIM_ENV_TAIL overrides; measured: DESIGN.md §6)
+constexpr uint32_t ENV_TAIL_DEFAULT = 8;
 constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);

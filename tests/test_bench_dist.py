@@ -127,7 +127,7 @@ def test_two_rank_bench_bookkeeping_on_cpu(tmp_path):
     assert r6["global_batch"] == 512 and r6["attractors"] == "fixture" and r6["update_cap"] == 4096
     assert "all_gather_GBs_per_gpu" in r6
     assert r6["high_cap"]["attractors"] == "fixture" and r6["high_cap"]["update_cap"] > 4096
-    assert r6["spec_attractors"]["attractors"] == "spec" and r6["spec_attractors"]["update_cap"] == 4096
+    assert r6["spec_attractors"]["attractors"] == "spec" and r6["spec_attractors"]["update_cap"] > 4096
 
 
 def test_failed_process_group_exits_nonzero_promptly():

@@ -718,13 +718,21 @@ def _random_cubes(rng, N, H, n_care):
                                   "syn300_wide_cube", "b28_first_tested", "b28_h12_first_tested",
                                   "tt200_first_tested", "b199_grp2", "b199_grp4", "b199_grp8", "b28_grp4_cap",
                                   "b28_grp8_first_tested", "b28_grp2_h8", "b199_grp4_long",
-                                  "b28_gen_cap41", "b199_gen_long", "b199_gen_long_first_tested"])
+                                  "b28_gen_cap41", "b199_gen_long", "b199_gen_long_first_tested",
+                                  "b28_gen_cap41_tail64", "b199_gen_long_tail64", "b199_gen_long_tail8",
+                                  "b199_gen_long_first_tested_tail64", "b28_first_tested_tail64", "b199_gen_long_tail0"])
 def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     """Every k_env variant (cooperative draw generation, byte counters without it, general
     cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs and
-    long until-attractor loops (thousands of updates per env step, odd caps)."""
+    long until-attractor loops (thousands of updates per env step, odd caps). ``_tailK``: the
+    cooperative-draw kernel's tail mode (a wave whose queue ran dry resolves its envs one at a time,
+    64 updates per block) from K live envs per wave (64: as soon as the queue is dry; 0: never;
+    the default is ENV_TAIL_DEFAULT)."""
     from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
 
+    if "_tail" in case:  # the same inputs as the base case, another tail-mode threshold
+        monkeypatch.setenv("PBNSIM_ENV_TAIL", case.split("_tail")[1])
+        case = case.split("_tail")[0]
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     cap, A, B = 3000, 3, 1024
     first = case.endswith("first_tested")  # PBNTargetEnv.step(force=False) semantics

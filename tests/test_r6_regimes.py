@@ -211,3 +211,43 @@ def test_collector_does_not_reuse_a_buffer_still_being_gathered(G):
     assert not torch.equal(expect[0], expect[2])
     for k in range(3):
         assert torch.equal(obs_snaps[k].view(expect[k].shape), expect[k]), k
+
+
+@pytest.mark.parametrize("spec", ["fixture", "spec"])
+def test_high_cap_matches_oracle(G, oracle_mod, spec):
+    """The loop the reference runs unbounded (pbn_target_multi.py:135-146) at a cap it never
+    reaches in measurement (bench.py R6_HIGH_CAP, 2^20; the longest loop measured at config 5 ran
+    78,057 updates, profiles/r03_r6_cap_sweep.json), for both attractor specs bench.py reports: the
+    fixture's cubes and SURVEY §8(d)'s 4 cubes over the 7 target genes. 8,192 envs x 3 env steps,
+    every env against the oracle; no env is capped."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    net = load_network("bittner199")
+    gnet = G.Net(net)
+    atts, _ = bench.r6_attractors(spec, net.n_nodes)
+    cfg = G.EnvConfig(gnet, atts, horizon=100)
+    cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
+                horizon=100)
+    B, seed, base, T, A = 8192, 0xAC7, 40000, 3, 4
+    b = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
+    b.env_reset(cfg)
+    o = oracle_mod.Oracle(net)
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
+                                cfg.reset_value, seed=seed, env_base=base, reset_count=0)
+    assert np.array_equal(b.get_state(), st)
+    acts = _actions(np.random.default_rng(123), (T, B, A), net.n_nodes)
+    for t in range(T):
+        obs, rew, flags, nup = b.env_step_multi(cfg, acts[t], update_cap=bench.R6_HIGH_CAP)
+        ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t,
+                               update_cap=bench.R6_HIGH_CAP)
+        assert np.array_equal(nup, ref["n_updates"]), t
+        assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), t
+        assert np.array_equal(flags, ref["flags"]), t
+        assert not (flags & 4).any()  # nothing reached the cap
+        st, ns = ref["state"], ref["n_steps"]
+    assert np.array_equal(b.get_state(), st)
+    b.close()
