@@ -750,53 +750,78 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                     const uint64_t w = wmask & below;
                     return w ? 63 - (int32_t)__clzll((long long)w) : -1;
                 };
-                bool fin = false, hitf = false;
-                while (!fin) {
-                    const uint32_t U = u + lane;  // this lane's update (blocks start at even indices)
+                // A block's draws, records, counter deltas and in-block writers do not depend on the
+                // state: prepared one block ahead (speculatively at u + 64: a block that does not end
+                // the env step always applies all 64 updates), under the current block's resolution.
+                struct TailDraw {
+                    uint4 q;
+                    uint32_t nd;
+                    uint64_t wi;
+                    int32_t r0, r1, r2, r3;
+                };
+                auto prepare = [&](uint32_t ub) {
+                    TailDraw D;
+                    const uint32_t U = ub + lane;
                     uint32_t w4[4];
                     philox_draw(a.seed, U >> 1, c1, gid, STREAM_ENV, w4);
                     const uint32_t odd = U & 1u;
                     const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
-                    const uint4 q = erec[__umul24(i, X.rs) + predictor_choice32(i, odd ? w4[3] : w4[1], lds, X.tp4)];
+                    D.q = erec[__umul24(i, X.rs) + predictor_choice32(i, odd ? w4[3] : w4[1], lds, X.tp4)];
                     constexpr uint32_t ROW = BLOCK * 4u;  // env_record's plane offsets: dword * ROW
-                    const uint32_t o0 = q.x & 0xFFFFu, o1 = q.x >> 16, o2 = q.y & 0xFFFFu, os = q.y >> 16;
-                    const uint32_t n0 = (o0 / ROW) * 32u | (q.z & 31u), n1 = (o1 / ROW) * 32u | ((q.z >> 8) & 31u),
-                                   n2 = (o2 / ROW) * 32u | ((q.z >> 16) & 31u), ss = (q.z >> 24) & 31u;
-                    // block-start values of the operands (in0, in1, in2, own bit)
-                    const uint32_t v0 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + o0), q.z, 1);
-                    const uint32_t v1 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + o1), q.z >> 8, 1);
-                    const uint32_t v2 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + o2), q.z >> 16, 1);
-                    const uint32_t v3 = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(colb + os), ss, 1);
+                    const uint32_t n0 = ((D.q.x & 0xFFFFu) / ROW) * 32u | (D.q.z & 31u),
+                                   n1 = ((D.q.x >> 16) / ROW) * 32u | ((D.q.z >> 8) & 31u),
+                                   n2 = ((D.q.y & 0xFFFFu) / ROW) * 32u | ((D.q.z >> 16) & 31u);
+                    D.nd = ndl[2u * i];
                     atomicOr(reinterpret_cast<unsigned long long*>(&wm[i]), 1ull << lane);
                     wave_sync();
-                    const uint64_t w0 = wm[n0], w1 = wm[n1], w2 = wm[n2], wi = wm[i];
+                    const uint64_t w0 = wm[n0], w1 = wm[n1], w2 = wm[n2];
+                    D.wi = wm[i];
                     wave_sync();
                     wm[i] = 0ull;  // the table is all zero again after every block
-                    const int32_t r0 = last_writer(w0), r1 = last_writer(w1), r2 = last_writer(w2),
-                                  r3 = last_writer(wi);
+                    D.r0 = last_writer(w0);
+                    D.r1 = last_writer(w1);
+                    D.r2 = last_writer(w2);
+                    D.r3 = last_writer(D.wi);
+                    return D;
+                };
+                bool fin = false, hitf = false;
+                TailDraw D = prepare(u);
+                while (!fin) {
+                    const uint4 q = D.q;
+                    const uint32_t U = u + lane;
+                    const uint32_t o0 = q.x & 0xFFFFu, o1 = q.x >> 16, o2 = q.y & 0xFFFFu, os = q.y >> 16;
+                    const uint32_t ss = (q.z >> 24) & 31u;
+                    // block-start values of the operands (in0, in1, in2, own bit)
+                    const uint32_t b0 = *reinterpret_cast<const uint32_t*>(colb + o0);
+                    const uint32_t b1 = *reinterpret_cast<const uint32_t*>(colb + o1);
+                    const uint32_t b2 = *reinterpret_cast<const uint32_t*>(colb + o2);
+                    const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + os);
+                    const TailDraw Dn = prepare(u + 64u);  // while those reads are in flight
+                    const uint32_t v0 = __builtin_amdgcn_ubfe(b0, q.z, 1), v1 = __builtin_amdgcn_ubfe(b1, q.z >> 8, 1),
+                                   v2 = __builtin_amdgcn_ubfe(b2, q.z >> 16, 1), v3 = __builtin_amdgcn_ubfe(b3, ss, 1);
                     uint32_t x3 = v3;
                     uint32_t y = __builtin_amdgcn_ubfe(q.w, (v0 << 3) | (v1 << 2) | (v2 << 1) | v3, 1);
-                    if (__ballot(r0 >= 0 || r1 >= 0 || r2 >= 0 || r3 >= 0) != 0) {
+                    if (__ballot(D.r0 >= 0 || D.r1 >= 0 || D.r2 >= 0 || D.r3 >= 0) != 0) {
                         for (;;) {
                             const uint64_t Y = __ballot(y != 0u);
                             auto pick = [&](int32_t r, uint32_t v) { return r >= 0 ? (uint32_t)(Y >> r) & 1u : v; };
-                            x3 = pick(r3, v3);
+                            x3 = pick(D.r3, v3);
                             const uint32_t yn = __builtin_amdgcn_ubfe(
-                                q.w, (pick(r0, v0) << 3) | (pick(r1, v1) << 2) | (pick(r2, v2) << 1) | x3, 1);
+                                q.w, (pick(D.r0, v0) << 3) | (pick(D.r1, v1) << 2) | (pick(D.r2, v2) << 1) | x3, 1);
                             if (__ballot(yn != y) == 0) break;
                             y = yn;
                         }
                     }
                     // packed counter deltas (+ d for 0 -> 1, - d for 1 -> 0), prefix over the block
                     const uint32_t sg = y - 1u;
-                    const uint32_t mk = m + wave_inclusive_add((((y ^ x3) ? ndl[2u * i] : 0u) ^ sg) - sg);
+                    const uint32_t mk = m + wave_inclusive_add((((y ^ x3) ? D.nd : 0u) ^ sg) - sg);
                     const bool valid = U < a.update_cap;
                     const bool hk = (U == 0u && !a.first_tested) ? h0 != 0u : has_zero_byte(mk) != 0u;
                     const uint64_t SM = __ballot(valid && hk), VM = __ballot(valid);
                     const uint32_t nd = SM ? (uint32_t)__ffsll((unsigned long long)SM) : (uint32_t)__popcll(VM);
                     const uint64_t within = nd >= 64u ? ~0ull : ((1ull << nd) - 1ull);
                     // commit: the last writer of each node among the first nd updates, if it changed the bit
-                    if (lane < nd && (wi & ~upto & within) == 0ull && y != v3) {
+                    if (lane < nd && (D.wi & ~upto & within) == 0ull && y != v3) {
                         uint32_t* dw = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + os);
                         if (y)
                             atomicOr(dw, 1u << ss);
@@ -807,6 +832,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
                     u += nd;
                     hitf = SM != 0ull;
                     fin = hitf || u >= a.update_cap;
+                    D = Dn;
                     wave_sync();
                 }
                 if (lane == L) {
