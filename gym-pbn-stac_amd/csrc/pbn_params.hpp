@@ -200,7 +200,7 @@ constexpr uint32_t ENV_CHUNK = PBN_ENV_CHUNK;  // updates per lane between refil
 constexpr uint32_t ENV_UNROLL = PBN_ENV_UNROLL;  // updates between the wave's "any lane active" tests
 // k_env tail mode: live envs per wave at (or below) which a wave whose queue ran dry switches to
 // resolving one env at a time across all 64 lanes (PBNSIM_ENV_TAIL overrides; measured: DESIGN.md §6)
-constexpr uint32_t ENV_TAIL_DEFAULT = 8;
+constexpr uint32_t ENV_TAIL_DEFAULT = 16;
 constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);

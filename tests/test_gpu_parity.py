@@ -719,15 +719,16 @@ def _random_cubes(rng, N, H, n_care):
                                   "tt200_first_tested", "b199_grp2", "b199_grp4", "b199_grp8", "b28_grp4_cap",
                                   "b28_grp8_first_tested", "b28_grp2_h8", "b199_grp4_long",
                                   "b28_gen_cap41", "b199_gen_long", "b199_gen_long_first_tested",
-                                  "b28_gen_cap41_tail64", "b199_gen_long_tail64", "b199_gen_long_tail8",
-                                  "b199_gen_long_first_tested_tail64", "b28_first_tested_tail64", "b199_gen_long_tail0"])
+                                  "b28_gen_cap41_tail32", "b199_gen_long_tail32", "b199_gen_long_tail16",
+                                  "b199_gen_long_tail8", "b199_gen_long_tail1", "b199_gen_long_first_tested_tail32",
+                                  "b28_first_tested_tail32", "b28_gen_cap41_tail3", "b199_gen_long_tail0"])
 def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     """Every k_env variant (cooperative draw generation, byte counters without it, general
     cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs and
     long until-attractor loops (thousands of updates per env step, odd caps). ``_tailK``: the
     cooperative-draw kernel's tail mode (a wave whose queue ran dry resolves its envs one at a time,
-    64 updates per block) from K live envs per wave (64: as soon as the queue is dry; 0: never;
-    the default is ENV_TAIL_DEFAULT)."""
+    64 updates per block) from K live envs per wave (32: early, many envs queued behind the one
+    resolved; 1: the last env only; 0: never; the default is ENV_TAIL_DEFAULT)."""
     from gym_pbn_amd.network import PredictorNetwork, synthetic_predictor_sets
 
     if "_tail" in case:  # the same inputs as the base case, another tail-mode threshold
