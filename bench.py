@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--rollout", type=int, default=64, help="updates per launch for the supplementary rollout line")
     p.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    p.add_argument("--valu-file", default=str(ROOT / "profiles" / "r02_valu_pmc.json"))
+    p.add_argument("--valu-file", default=str(ROOT / "profiles" / "r03_valu_pmc.json"))
     p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
     p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
     p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
@@ -342,7 +342,7 @@ def rollout_supplement(net, B, device, seed, T, valu):
 
 def valu_roofline(v, s, updates):
     """VALU roofline: VALU wave-instructions per node update from committed SQ counters
-    (profiles/r02_valu_pmc.json, tools/valu_pmc.py: SQ_INSTS_VALU over a profiled launch of the
+    (profiles/r03_valu_pmc.json, tools/valu_pmc.py: SQ_INSTS_VALU over a profiled launch of the
     same kernel, batch and seeds / its node updates) x this run's node updates / its kernel time,
     against the chip's VALU issue peak (64 lanes per wave-instruction)."""
     ipu = v["valu_wave_insts_per_update"]
@@ -350,7 +350,7 @@ def valu_roofline(v, s, updates):
     return {"bound": "valu", "achieved": lane_ops / s / 1e12, "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
             "frac": lane_ops / s / 1e12 / VALU_PEAK_TOPS, "valu_wave_insts_per_update": ipu,
             "valu_busy_frac": v.get("valu_busy_frac"), "kernel_s": s, "node_updates": updates,
-            "source": v.get("source", "profiles/r02_valu_pmc.json")}
+            "source": v.get("source", "profiles/r03_valu_pmc.json")}
 
 
 def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather=True):

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r02_valu_pmc.json (copied to
+"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r03_valu_pmc.json (copied to
 profiles/ after review; bench.py reads it for the rollout and config-5 rooflines).
 
 One rocprofv3 --pmc pass (kernel trace only; 4 SQ counters + 1 GRBM counter, within one pass's
@@ -62,7 +62,7 @@ def main():
                     "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
     doc = {"kernels": res, "valu_peak": "256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s "
                                         "(MI355X_MICROARCH.md: chip parameters, wave scheduling)"}
-    (ROOT / "gpurun_out" / "r02_valu_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
+    (ROOT / "gpurun_out" / "r03_valu_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps({k: {kk: v[kk] for kk in ("valu_wave_insts_per_update", "valu_busy_frac", "effective_clock_GHz",
                                                "launches")} for k, v in res.items()}))
 
