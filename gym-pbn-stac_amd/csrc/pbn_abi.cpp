@@ -151,6 +151,7 @@ struct pbn_batch {
     uint32_t env_calls = 0, reset_count = 0;
     int env_lanes = 0;  // lanes per env of the last R6 launch
     int env_grid_last = 0;  // workgroups of the last R6 launch
+    int env_lane_limit_last = 0;  // lanes per wave taking envs in the last R6 launch
     int env_kernel_last = -1;  // pbn_batch_info.env_kernel of the last R6 launch
     uint64_t* d_state = nullptr;
     int64_t* d_nsteps = nullptr;
@@ -166,6 +167,7 @@ struct pbn_batch {
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
     int env_grid_cap = 0;     // PBNSIM_ENV_GRID: cap on the R6 kernel's workgroups (tests: lane refill), 0 = none
     int env_tail = -1;        // PBNSIM_ENV_TAIL: the R6 kernel's tail-mode threshold (live envs per wave), -1 = default
+    int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
@@ -518,6 +520,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_GRID")) b->env_grid_cap = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_TAIL")) b->env_tail = std::max(0, std::min(64, atoi(v)));
+    if (const char* v = getenv("PBNSIM_ENV_LANES")) b->env_lane_limit = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -610,6 +613,7 @@ int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
     info->roll_lanes = b->roll_group;
     info->env_grid = b->env_grid_last;
     info->env_kernel = b->env_kernel_last;
+    info->env_lane_limit = b->env_lane_limit_last;
     return 0;
 }
 
@@ -1324,7 +1328,11 @@ int pbn_get_n_steps(pbn_batch* b, int64_t* n_steps) {
 // Per-step call, Bittner-200, 1 MI355X (256 CUs): G = 8 beats lane mode up to 32k envs (0.21 vs
 // 0.33 ms at B = 1, 0.88 vs 1.99 ms at 8k, 1.85 vs 2.04 ms at 32k) and loses from 64k on (2.31 vs
 // 2.07 ms; 131k: 3.28 vs 2.60 ms) -- the crossover sits near 48k envs.
-static int env_group_size(const pbn_batch* b) {
+// Group mode (G = 8 lanes per env) for small batches -- except with <= 4 cubes, where the lane
+// kernel's tail mode with one env per wave (env_lane_limit) is faster at every batch size measured
+// (profiles/r03_r6_lanes_sweep.json)
+static int env_group_size(const pbn_batch* b, int n_cubes) {
+    if (n_cubes <= 4) return 1;
     return b->B * 8 <= (uint64_t)b->n_cu * 1536 ? 8 : 1;
 }
 
@@ -1341,7 +1349,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     // group mode (k_env_grp: G lanes per env, G updates per round trip)
     int grp = 1;
     if (mode == 2 && b->net->N <= 256) {
-        grp = b->env_group ? b->env_group : env_group_size(b);
+        grp = b->env_group ? b->env_group : env_group_size(b, cfg->H);
         if (grp != 2 && grp != 4 && grp != 8) grp = 1;
         if (grp > 1) mode = 3;
     }
@@ -1380,6 +1388,17 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.off_ndelta = cfg->off_ndelta + erec_shift;
     a.erec_shift = erec_shift;
     a.tail_max = b->env_tail >= 0 ? (uint32_t)b->env_tail : ENV_TAIL_DEFAULT;
+    // tail-mode kernel: small batches (ENV_ONE_LANE_ENVS_PER_SLOT envs per wave slot) take one env per
+    // wave at a time -- every wave resolves its env 64 updates per block and takes the next from the
+    // queue when it is done (PBNSIM_ENV_LANES overrides; 64 = lane mode, the tail at the end)
+    a.lane_limit = 64u;
+    if (mode == 4) {
+        const uint64_t slots = (uint64_t)b->n_cu * (uint64_t)bpc * (BLOCK / 64);
+        if (b->env_lane_limit > 0)
+            a.lane_limit = (uint32_t)b->env_lane_limit;
+        else if (a.tail_max >= 1 && b->B <= ENV_ONE_LANE_ENVS_PER_SLOT * slots)
+            a.lane_limit = 1u;
+    }
     a.fast = mode;
     a.grp = grp;
     a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + erec_shift + 8u * (uint32_t)b->W * BLOCK;
@@ -1406,7 +1425,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     HIP_TRY(hipMemsetAsync(b->s_counter.p, 0, 8, b->stream));
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
-    int grid = b->grid_for(b->B * (uint64_t)grp, bpc);
+    // lanes per env (group mode) or, with a lane limit, 64 / limit lane slots per env
+    int grid = b->grid_for(a.lane_limit < 64u ? (b->B * 64u + a.lane_limit - 1u) / a.lane_limit : b->B * (uint64_t)grp, bpc);
     if (b->env_grid_cap) grid = std::min(grid, b->env_grid_cap);  // persistent waves: any grid drains the counter
     int e = launch_env_multi(b->W, a, replay, grid, b->stream);
     if (e) return fail(PBN_E_HIP, "k_env launch: %s", hipGetErrorString((hipError_t)e));
@@ -1414,6 +1434,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     if (!replay) b->env_calls += n_calls;
     b->env_lanes = grp;
     b->env_grid_last = grid;
+    b->env_lane_limit_last = (int)a.lane_limit;
     b->env_kernel_last = replay ? std::min(mode, 1) : mode;
     return 0;
 }

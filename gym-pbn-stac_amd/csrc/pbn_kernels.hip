@@ -603,7 +603,7 @@ __global__ __launch_bounds__(BLOCK) void k_env(EnvArgs a) {
 
     int64_t e = -1;
     uint32_t t = 0;  // env step of this launch the lane is on (a.n_calls steps per env)
-    bool exhausted = false;
+    bool exhausted = TAIL && lane >= a.lane_limit;  // lanes past the limit take no env
     uint64_t o0[W];
     uint32_t m_lo = 0, m_hi = 0;  // FAST: packed per-cube mismatch counters
     bool hit0 = false;            // o0 is attracting (the test made after the first update)

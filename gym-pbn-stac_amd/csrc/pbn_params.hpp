@@ -114,6 +114,8 @@ struct EnvArgs {
                               // (off_cubes / off_target / off_ndelta / off_gen are LDS offsets)
     uint32_t tail_max;        // fast == 4: a wave whose queue ran dry resolves its envs one at a time,
                               // 64 updates per block, once it holds at most this many (0 = never)
+    uint32_t lane_limit;      // fast == 4: lanes per wave that take envs from the work queue (64 = all;
+                              // <= tail_max: every wave in tail mode from its first env)
 };
 
 constexpr uint32_t MT_ROW = 624;
@@ -201,6 +203,13 @@ constexpr uint32_t ENV_UNROLL = PBN_ENV_UNROLL;  // updates between the wave's "
 // k_env tail mode: live envs per wave at (or below) which a wave whose queue ran dry switches to
 // resolving one env at a time across all 64 lanes (PBNSIM_ENV_TAIL overrides; measured: DESIGN.md §6)
 constexpr uint32_t ENV_TAIL_DEFAULT = 16;
+// Batches of up to this many envs per wave slot (n_cu x workgroups per CU x 4 waves: 3,072 for
+// Bittner-200 on 256 CUs): one lane per wave takes envs (EnvArgs::lane_limit = 1), so every wave
+// works in tail mode on one env at a time and takes the next from the queue. Measured against lane
+// mode (profiles/r03_r6_lanes_sweep.json): faster or tied on every line up to 16,384 envs (5.3 per
+// slot; e.g. 8,192 envs, cap 4,096: 0.19 vs 0.96 ms per step); at 32,768 the spec attractors' per-step
+// line is 31 % slower (short env steps queue behind long ones in one wave), so 6 per slot
+constexpr uint64_t ENV_ONE_LANE_ENVS_PER_SLOT = 6;
 constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);

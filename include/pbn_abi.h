@@ -86,6 +86,8 @@ typedef struct {
     int32_t env_grid;   /* last R6 env-step launch: workgroups (256 lanes each; lanes refill from a work counter) */
     int32_t env_kernel; /* last R6 env-step launch: 0 = cube matching, 1 = byte counters, 2 = byte counters +
                            wave-generated draws, 3 = group mode (k_env_grp), 4 = 2 with one counter word (<= 4 cubes) */
+    int32_t env_lane_limit; /* last R6 env-step launch, env_kernel 4: lanes per wave taking envs from the work
+                               queue (64 = every lane; 1 = one env per wave at a time, resolved 64 updates per block) */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).

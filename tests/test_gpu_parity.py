@@ -5,6 +5,7 @@ oracle to finish in seconds; the 1M-env cases check size-independent
 properties (shard invariance, step == rollout, sampled envs vs the oracle).
 """
 
+import os
 import zlib
 
 import numpy as np
@@ -721,7 +722,9 @@ def _random_cubes(rng, N, H, n_care):
                                   "b28_gen_cap41", "b199_gen_long", "b199_gen_long_first_tested",
                                   "b28_gen_cap41_tail32", "b199_gen_long_tail32", "b199_gen_long_tail16",
                                   "b199_gen_long_tail8", "b199_gen_long_tail1", "b199_gen_long_first_tested_tail32",
-                                  "b28_first_tested_tail32", "b28_gen_cap41_tail3", "b199_gen_long_tail0"])
+                                  "b28_first_tested_tail32", "b28_gen_cap41_tail3", "b199_gen_long_tail0",
+                                  "b199_gen_long_lanes16", "b199_gen_long_lanes1", "b28_gen_cap41_lanes4",
+                                  "b199_gen_long_first_tested_lanes8"])
 def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     """Every k_env variant (cooperative draw generation, byte counters without it, general
     cube matching, truth-table kind, W = 8) against the oracle's R6 step, incl. capped envs and
@@ -734,6 +737,12 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
     if "_tail" in case:  # the same inputs as the base case, another tail-mode threshold
         monkeypatch.setenv("PBNSIM_ENV_TAIL", case.split("_tail")[1])
         case = case.split("_tail")[0]
+    # lane mode proper (every lane takes envs) unless the case names K lanes per wave taking envs
+    # (tail mode from the first env; batches this small default to K = 1)
+    monkeypatch.setenv("PBNSIM_ENV_LANES", "64")
+    if "_lanes" in case:
+        monkeypatch.setenv("PBNSIM_ENV_LANES", case.split("_lanes")[1])
+        case = case.split("_lanes")[0]
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     cap, A, B = 3000, 3, 1024
     first = case.endswith("first_tested")  # PBNTargetEnv.step(force=False) semantics
@@ -796,6 +805,7 @@ def test_env_kernel_variants_match_oracle(G, oracle_mod, monkeypatch, case):
             assert b.info()["env_lanes"] == int(case.split("_grp")[1][0])  # group mode really ran
         if case in ("b28_gen_cap", "b28_first_tested", "b28_gen_cap41") or case.startswith("b199_gen_long"):
             assert b.info()["env_kernel"] == 4  # wave-generated draws, one counter word (<= 4 cubes)
+            assert b.info()["env_lane_limit"] == int(os.environ["PBNSIM_ENV_LANES"])
         if case in ("b28_h8_gen", "b199_h6_gen_first_tested"):
             assert b.info()["env_kernel"] == 2  # wave-generated draws, two counter words
     if case in ("b28_gen_cap", "b28_grp4_cap", "b199_grp4_long", "b28_gen_cap41") or case.startswith("b199_gen_long"):

@@ -51,12 +51,15 @@ def G():
     return batch
 
 
-@pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step"])
+@pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step", "one_lane_per_step", "one_lane_fused"])
 def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
     import torch
 
     grp = "8" if mode.startswith("grp8") else "1"
     monkeypatch.setenv("PBNSIM_ENV_GROUP", grp)
+    # every lane takes envs (lane mode proper), or one lane per wave (tail mode from the first env,
+    # each wave taking its next env from the queue when one ends)
+    monkeypatch.setenv("PBNSIM_ENV_LANES", "1" if mode.startswith("one_lane") else "64")
     grid = 4 if grp == "1" else 2
     monkeypatch.setenv("PBNSIM_ENV_GRID", str(grid))
     B = 6144 if grp == "1" else 1024
@@ -69,7 +72,7 @@ def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
                                 cfgd["reset_value"], seed=seed, env_base=base, reset_count=0)
     assert np.array_equal(b.get_state(), st)
     acts = _actions(np.random.default_rng(17), (T, B, A), net.n_nodes)
-    if mode == "fused":
+    if mode.endswith("fused"):
         dev = torch.device("cuda", 0)
         d_a = torch.from_numpy(acts).to(dev)
         o_ = torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev)
@@ -85,6 +88,8 @@ def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
         got = [b.env_step_multi(cfg, acts[t], update_cap=CAP) for t in range(T)]
     info = b.info()
     assert info["env_grid"] == grid and info["env_lanes"] == int(grp)
+    if grp == "1":
+        assert info["env_kernel"] == 4 and info["env_lane_limit"] == (1 if mode.startswith("one_lane") else 64)
     capped = 0
     for t in range(T):
         ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=CAP)
