@@ -208,12 +208,70 @@ __device__ __forceinline__ void k_step_single(const StepArgs& a, uint8_t* lds, u
 #endif
 }
 
+// The bench shape: every thread owns exactly one env pair (B <= 2 x grid x SB), image staged and both
+// loads issued by k_step. Straight-line, so both envs' threshold rows are read in one LDS round trip
+// and both records in a second (the looped form read env 0's row, its record, env 1's row, its
+// record: three dependent round trips, the uniform tp4 == 4 branch between them), and env 0's plane
+// work waits only for env 0's loads.
+template <int W, int SB>
+__device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uint64_t e, uint64_t stride,
+                                            const uint64_t (&cur)[W], const uint64_t (&nxt)[W], uint32_t N) {
+    const uint64_t u = a.update_base + (a.ubase_dev ? *a.ubase_dev : 0ull);
+    const uint64_t e1 = e + stride, g0 = a.env_base + e, g1 = g0 + stride;
+    uint32_t n0, c0, n1, c1;
+    if ((a.env_base & 1u) == 0u) {  // envs 2m / 2m + 1 share a Philox call (k_step_single)
+        step_words_paired(a.seed, u, g0, g1, (threadIdx.x & 1u) != 0u, n0, c0, n1, c1);
+    } else {
+        step_words(a.seed, u, g0, n0, c0);
+        step_words(a.seed, u, g1, n1, c1);
+    }
+    const uint32_t i0 = philox_node<KIND_PREDICTOR_MIX>(n0, N), i1 = philox_node<KIND_PREDICTOR_MIX>(n1, N);
+    const Thr32 X = thr32_layout(a.L);
+    uint32_t j0, j1;
+    if (X.tp4 == 4u) {
+        const uint4 t0 = reinterpret_cast<const uint4*>(lds)[i0];
+        const uint4 t1 = reinterpret_cast<const uint4*>(lds)[i1];
+        j0 = (c0 >= t0.x ? 1u : 0u) + (c0 >= t0.y ? 1u : 0u) + (c0 >= t0.z ? 1u : 0u) + (c0 >= t0.w ? 1u : 0u);
+        j1 = (c1 >= t1.x ? 1u : 0u) + (c1 >= t1.y ? 1u : 0u) + (c1 >= t1.z ? 1u : 0u) + (c1 >= t1.w ? 1u : 0u);
+    } else {
+        j0 = predictor_choice32(i0, c0, lds, X.tp4);
+        j1 = predictor_choice32(i1, c1, lds, X.tp4);
+    }
+    const uint64_t* rec = reinterpret_cast<const uint64_t*>(lds + X.rec_off);
+    const uint64_t r0 = rec[i0 * X.rs + j0], r1 = rec[i1 * X.rs + j1];
+    const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.plane_off) + threadIdx.x};
+    const bool last_dw = N > 64u * W - 32u;  // the plane's last dword holds nodes >= 64W - 32 only
+    auto eval = [&](const uint64_t (&s)[W], uint32_t i, uint64_t r, uint32_t& self) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            P.put(2 * k, (uint32_t)s[k]);
+            if (k + 1 < W || last_dw) P.put(2 * k + 1, (uint32_t)(s[k] >> 32));
+        }
+        self = P.get(i >> 5);
+        return predictor_apply(P, i, self, r);
+    };
+    uint32_t self0, self1;
+    const uint32_t y0 = eval(cur, i0, r0, self0);
+    const uint32_t y1 = eval(nxt, i1, r1, self1);  // past B: junk from a clamped load, never stored
+    auto put = [&](const uint64_t (&s)[W], uint64_t eh, uint32_t i) {  // whole env, bit i flipped
+        uint64_t out[W];
+        const uint32_t wi = i >> 6;
+        const uint64_t m = 1ull << (i & 63u);
+#pragma unroll
+        for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
+        store_state<W>(a.state + eh * W, out);
+    };
+    if (e < a.B && ((self0 >> (i0 & 31u)) & 1u) != y0) put(cur, e, i0);
+    if (e1 < a.B && ((self1 >> (i1 & 31u)) & 1u) != y1) put(nxt, e1, i1);
+}
+
 // Step mode (T == 1, Philox; REPLAY == 0) and replay mode (REPLAY == 1: T updates from the
 // caller's draws). Rollout (T > 1, Philox) is its own kernel, k_rollout, so that neither
 // path's code shapes the other's register allocation and schedule (sharing one kernel cost
 // the step path 0.6 us per launch at 1M envs).
 template <int W, int KIND, int STORE, int REPLAY, int SB>
-__global__ __launch_bounds__(SB)
+// 1024-thread groups, W <= 4: two workgroups per CU = 8 waves per SIMD, so at most 64 VGPRs
+__global__ __launch_bounds__(SB, (SB == 1024 && W <= 4) ? 8 : 1)
 #ifdef PBN_STAMPS
 __attribute__((amdgpu_waves_per_eu(8, 8)))  // the product's occupancy (64 VGPRs) despite the stamps
 #endif
@@ -242,7 +300,10 @@ void k_step(StepArgs a) {
         if (threadIdx.x < n16) reinterpret_cast<uint4*>(lds)[threadIdx.x] = g;
         for (uint32_t k = threadIdx.x + SB; k < n16; k += SB) reinterpret_cast<uint4*>(lds)[k] = src[k];
         __syncthreads();
-        k_step_single<W, KIND, STORE, SB, true>(a, lds, e, stride, cur, N, &nx);
+        if (STORE == STORE_DIRTY && 2u * stride >= a.B)
+            k_step_pair<W, SB>(a, lds, e, stride, cur, nx, N);  // one pair per thread (the bench shape)
+        else
+            k_step_single<W, KIND, STORE, SB, true>(a, lds, e, stride, cur, N, &nx);
         return;
     }
     if (e < a.B) load_state<W>(a.state + e * W, cur);
