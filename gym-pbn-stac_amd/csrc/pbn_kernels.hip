@@ -250,9 +250,6 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
         self = P.get(i >> 5);
         return predictor_apply(P, i, self, r);
     };
-    uint32_t self0, self1;
-    const uint32_t y0 = eval(cur, i0, r0, self0);
-    const uint32_t y1 = eval(nxt, i1, r1, self1);  // past B: junk from a clamped load, never stored
     auto put = [&](const uint64_t (&s)[W], uint64_t eh, uint32_t i) {  // whole env, bit i flipped
         uint64_t out[W];
         const uint32_t wi = i >> 6;
@@ -261,7 +258,14 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
         for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
         store_state<W>(a.state + eh * W, out);
     };
+    uint32_t self0, self1;
+    const uint32_t y0 = eval(cur, i0, r0, self0);
+    // env 0 is stored before env 1 is evaluated; env 1's loads (issued right behind env 0's) are waited
+    // for first: after a store that may not have been issued, the compiler can only wait vmcnt(0)
+#pragma unroll
+    for (int k = 0; k < W; ++k) asm volatile("" ::"v"(nxt[k]));
     if (e < a.B && ((self0 >> (i0 & 31u)) & 1u) != y0) put(cur, e, i0);
+    const uint32_t y1 = eval(nxt, i1, r1, self1);  // past B: junk from a clamped load, never stored
     if (e1 < a.B && ((self1 >> (i1 & 31u)) & 1u) != y1) put(nxt, e1, i1);
 }
 
