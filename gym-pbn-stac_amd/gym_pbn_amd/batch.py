@@ -398,6 +398,12 @@ class PBNBatch:
         L.check(L.lib.pbn_timing_read(self._h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def env_handoffs(self) -> int:
+        """Envs the last R6 launch handed from tail-mode waves to idle ones (0 with the hand-off off)."""
+        n = C.c_uint32(0)
+        L.check(L.lib.pbn_env_handoffs(self._h, C.byref(n)))
+        return n.value
+
 
 __all__ = ["Net", "EnvConfig", "PBNBatch", "pack_bits", "unpack_bits", "cube_arrays", "attractors_from_cubes",
            "KIND_PREDICTOR_MIX"]

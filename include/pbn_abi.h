@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 11
+#define PBN_ABI_VERSION 12
 
 enum {
     PBN_OK = 0,
@@ -88,6 +88,8 @@ typedef struct {
                            wave-generated draws, 3 = group mode (k_env_grp), 4 = 2 with one counter word (<= 4 cubes) */
     int32_t env_lane_limit; /* last R6 env-step launch, env_kernel 4: lanes per wave taking envs from the work
                                queue (64 = every lane; 1 = one env per wave at a time, resolved 64 updates per block) */
+    int32_t env_handoff;    /* last R6 env-step launch, env_kernel 4: 1 if waves in tail mode could hand envs
+                               to idle waves (on with PBNSIM_ENV_STEAL=1); count: pbn_env_handoffs */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).
@@ -242,6 +244,10 @@ int pbn_ssd_run(pbn_batch *b, const int32_t *target_nodes, int n_targets, const 
  *      mode 2: one region from before the first launch to after the last (launch gaps included) ---- */
 int pbn_timing_enable(pbn_batch *b, int enable);
 int pbn_timing_read(pbn_batch *b, double *kernel_ms, uint64_t *launches); /* syncs, then resets */
+/* Envs handed from a tail-mode wave to an idle one during the last R6 env-step launch (env_kernel 4;
+ * 0 when the hand-off was off). Syncs the batch stream. Diagnostics: the reference has no counterpart
+ * (its until-attractor loop, pbn_target_multi.py:135-146, runs one env in one process). */
+int pbn_env_handoffs(pbn_batch *b, uint32_t *count);
 
 #ifdef __cplusplus
 }

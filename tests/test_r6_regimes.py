@@ -256,3 +256,69 @@ def test_high_cap_matches_oracle(G, oracle_mod, spec):
         st, ns = ref["state"], ref["n_steps"]
     assert np.array_equal(b.get_state(), st)
     b.close()
+
+
+@pytest.mark.parametrize("mode", ["per_step", "fused"])
+def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, mode):
+    """Tail envs handed from wave to wave (k_env mode 4, ``EnvArgs::steal``): at the reference's
+    unbounded-loop cap (2^20) one wave's long until-attractor loops would run one after another in
+    its tail while waves whose envs all ended sit idle, so tail waves pass envs (registers + plane
+    column, through device-memory slots) to idle waves, which resume them in lane 0. 32 workgroups
+    (128 waves) hold one env per lane; the launch must hand envs off, and every env of every step
+    equals the oracle (obs, reward, flags, update counts, final state and step counters)."""
+    import torch
+
+    monkeypatch.setenv("PBNSIM_ENV_LANES", "64")
+    monkeypatch.setenv("PBNSIM_ENV_GRID", "32")
+    monkeypatch.setenv("PBNSIM_ENV_STEAL", "1")
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    net = load_network("bittner199")
+    gnet = G.Net(net)
+    atts, _ = bench.r6_attractors("fixture", net.n_nodes)
+    cfg = G.EnvConfig(gnet, atts, horizon=100)
+    cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
+                horizon=100)
+    B, seed, base, T, A = 8192, 0x5EED, 70001, 3, 4
+    cap = bench.R6_HIGH_CAP
+    b = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
+    b.env_reset(cfg)
+    o = oracle_mod.Oracle(net)
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
+                                cfg.reset_value, seed=seed, env_base=base, reset_count=0)
+    acts = _actions(np.random.default_rng(321), (T, B, A), net.n_nodes)
+    handed = []
+    if mode == "fused":
+        dev = torch.device("cuda", 0)
+        d_a = torch.from_numpy(acts).to(dev)
+        o_ = torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev)
+        r_ = torch.empty((T, B), dtype=torch.int32, device=dev)
+        f_ = torch.empty((T, B), dtype=torch.uint8, device=dev)
+        n_ = torch.empty((T, B), dtype=torch.int32, device=dev)
+        b.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, o_.data_ptr(), r_.data_ptr(), f_.data_ptr(),
+                                   n_.data_ptr(), update_cap=cap)
+        handed.append(b.env_handoffs())
+        got = [(o_[t].cpu().numpy().view(np.uint64), r_[t].cpu().numpy(), f_[t].cpu().numpy(),
+                n_[t].cpu().numpy().view(np.uint32)) for t in range(T)]
+    else:
+        got = []
+        for t in range(T):
+            got.append(b.env_step_multi(cfg, acts[t], update_cap=cap))
+            handed.append(b.env_handoffs())
+    info = b.info()
+    assert info["env_kernel"] == 4 and info["env_lane_limit"] == 64 and info["env_grid"] == 32
+    assert info["env_handoff"] == 1
+    assert sum(handed) > 0, handed  # the hand-off path ran
+    for t in range(T):
+        ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=cap)
+        obs, rew, flags, nup = got[t]
+        assert np.array_equal(nup, ref["n_updates"]), t
+        assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), t
+        assert np.array_equal(flags, ref["flags"]), t
+        st, ns = ref["state"], ref["n_steps"]
+    assert np.array_equal(b.get_state(), st) and np.array_equal(b.get_n_steps(), ns)
+    b.close()

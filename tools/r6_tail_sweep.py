@@ -4,8 +4,9 @@ wave; 0 = off). Bittner-200, bench.py's config-5 settings (A = 4, 0 w.p. 0.75, h
 mode (PBNSIM_ENV_GROUP=1), both attractor specs and both caps; per batch size B: T env steps as
 one fused launch and as T per-step launches, ms per env step (best of 2). Measurement only.
 
-Usage: python tools/r6_tail_sweep.py B[,B...] TAIL[:LANES][,...] [T] [spec:cap,...]
-(LANES: PBNSIM_ENV_LANES, lanes per wave that take envs; 0 or absent = the library default.)
+Usage: python tools/r6_tail_sweep.py B[,B...] TAIL[:LANES[:STEAL]][,...] [T] [spec:cap,...]
+(LANES: PBNSIM_ENV_LANES, lanes per wave that take envs; 0 or absent = the library default.
+STEAL: PBNSIM_ENV_STEAL, hand-off of tail envs between waves, 1 = on (default) / 0 = off.)
 Output of `python tools/r6_tail_sweep.py 1,64,131072 0,2,8,64 10` -> profiles/r03_r6_tail_sweep.json."""
 import json
 import os
@@ -55,11 +56,13 @@ def child(B, T, spec, cap):
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         inf = b.info()
+        handoffs = b.env_handoffs()
         b.close()
         n = outs[3].to(torch.int64)
         res["fused" if fused else "per_step"] = {"ms_per_env_step": best * 1e3 / T, "env_steps_per_s": B * T / best,
                                                  "max_updates": int(n.max()), "mean_updates": float(n.float().mean()),
-                                                "env_grid": inf["env_grid"], "env_lane_limit": inf["env_lane_limit"]}
+                                                "env_grid": inf["env_grid"], "env_lane_limit": inf["env_lane_limit"],
+                                                "handoffs_last_launch": handoffs}
     print(json.dumps(res))
 
 
@@ -68,21 +71,24 @@ def main():
         child(int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], int(sys.argv[5]))
         return
     Bs = [int(x) for x in sys.argv[1].split(",")]
-    tails = [(int(x.split(":")[0]), int(x.split(":")[1]) if ":" in x else 0) for x in sys.argv[2].split(",")]
+    tails = [tuple(int(v) for v in (x.split(":") + ["0", "1"][len(x.split(":")) - 1:])[:3])
+             for x in sys.argv[2].split(",")]
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     specs = [(s.split(":")[0], int(s.split(":")[1])) for s in sys.argv[4].split(",")] if len(sys.argv) > 4 \
         else [("fixture", 4096), ("fixture", 1 << 20), ("spec", 1 << 20)]
     out = []
     for spec, cap in specs:
         for B in Bs:
-            for tail, lanes in tails:
-                env = dict(os.environ, PBNSIM_ENV_GROUP="1", PBNSIM_ENV_TAIL=str(tail), PBNSIM_ENV_LANES=str(lanes))
+            for tail, lanes, steal in tails:
+                env = dict(os.environ, PBNSIM_ENV_GROUP="1", PBNSIM_ENV_TAIL=str(tail), PBNSIM_ENV_LANES=str(lanes),
+                           PBNSIM_ENV_STEAL=str(steal))
                 p = subprocess.run([sys.executable, __file__, "--child", str(B), str(T), spec, str(cap)], env=env,
                                    capture_output=True, text=True, timeout=300)
                 if p.returncode:
                     print(p.stderr[-2000:], file=sys.stderr)
                     sys.exit(p.returncode)
-                row = {"attractors": spec, "update_cap": cap, "B": B, "tail_max": tail, "lanes": lanes or "auto", "T": T,
+                row = {"attractors": spec, "update_cap": cap, "B": B, "tail_max": tail, "lanes": lanes or "auto",
+                       "steal": steal, "T": T,
                        **json.loads(p.stdout.strip().splitlines()[-1])}
                 print(json.dumps(row), flush=True)
                 out.append(row)
