@@ -168,7 +168,7 @@ struct pbn_batch {
     int env_grid_cap = 0;     // PBNSIM_ENV_GRID: cap on the R6 kernel's workgroups (tests: lane refill), 0 = none
     int env_tail = -1;        // PBNSIM_ENV_TAIL: the R6 kernel's tail-mode threshold (live envs per wave), -1 = default
     int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
-    bool env_steal = false;   // PBNSIM_ENV_STEAL=1: hand-off of tail envs between waves (k_env, mode 4)
+    bool env_steal = true;    // PBNSIM_ENV_STEAL=0: no hand-off of tail envs between a workgroup's waves (k_env, mode 4)
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
@@ -197,8 +197,7 @@ struct pbn_batch {
     DevBuf s_act, s_obs, s_rew, s_flags, s_nup, s_replay_i, s_replay_k, s_off, s_mask;
     DevBuf mt_py, mt_np, mt_pos_py, mt_pos_np, mt_seeds;  // MT mode (allocated by pbn_mt_seed)
     DevBuf s_counter;                                     // env-step work-queue head
-    DevBuf s_steal;                                       // k_env tail hand-off: control words + slots
-    uint32_t steal_seq = 0;                               // tag of the last launch's slots
+    DevBuf s_steal;                                       // k_env tail hand-off: count of envs handed off
     bool steal_last = false;                              // the last R6 launch had the hand-off on
     PinBuf pin;                                           // staging for small host<->device copies
     DevBuf s_ssd_hist, s_ssd_tab;                         // SSD histogram + gap/target tables
@@ -1432,27 +1431,15 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     // lanes per env (group mode) or, with a lane limit, 64 / limit lane slots per env
     int grid = b->grid_for(a.lane_limit < 64u ? (b->B * 64u + a.lane_limit - 1u) / a.lane_limit : b->B * (uint64_t)grp, bpc);
     if (b->env_grid_cap) grid = std::min(grid, b->env_grid_cap);  // persistent waves: any grid drains the counter
-    // tail hand-off (k_env mode 4): waves that hold several envs in tail mode pass envs to idle waves.
-    // One lane per wave taking envs (small batches) never holds two: off there. Pull tickets: a wave
-    // takes one each time it runs out of envs, so at most one per wave plus one per env handed off
-    // (at most 16 per wave of the grid; an env is handed off at most once: its new wave holds no other)
+    // tail hand-off (k_env mode 4): a wave holding several envs in tail mode passes envs it has not
+    // started on to idle waves of its workgroup (LDS). One lane per wave taking envs (small batches)
+    // never holds two: off there
     b->steal_last = false;
     if (mode == 4 && b->env_steal && a.tail_max >= 1u && a.lane_limit >= 2u) {
-        const uint64_t waves = (uint64_t)grid * (BLOCK / 64);
-        const uint32_t push_cap = (uint32_t)std::min<uint64_t>(b->B, 16u * waves);
-        const uint32_t cap = push_cap + (uint32_t)waves + 64u;
-        const size_t before = b->s_steal.cap;
-        if (int rc = b->s_steal.ensure(8 * (STEAL_CTL_WORDS + (size_t)cap * STEAL_SLOT_WORDS))) return rc;
-        if (b->s_steal.cap != before) {  // fresh slots: no tag of an earlier launch
-            HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, b->s_steal.cap, b->stream));
-            b->steal_seq = 0;
-        }
-        if (++b->steal_seq == 0u) ++b->steal_seq;
-        HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, 8 * STEAL_CTL_WORDS, b->stream));
-        a.steal = (uint64_t*)b->s_steal.p;
-        a.steal_cap = cap;
-        a.steal_push_cap = push_cap;
-        a.steal_seq = b->steal_seq;
+        if (int rc = b->s_steal.ensure(8)) return rc;
+        HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, 4, b->stream));
+        a.steal_local = 1;
+        a.steal_count = (uint32_t*)b->s_steal.p;
         b->steal_last = true;
     }
     hipEvent_t stop;
@@ -1643,7 +1630,7 @@ int pbn_env_handoffs(pbn_batch* b, uint32_t* count) {
     *count = 0;
     if (!b->steal_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
-    HIP_TRY(hipMemcpy(count, b->s_steal.p, 4, hipMemcpyDeviceToHost));  // the push half of the ticket word
+    HIP_TRY(hipMemcpy(count, b->s_steal.p, 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

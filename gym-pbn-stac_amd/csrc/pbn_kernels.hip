@@ -603,27 +603,6 @@ __device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
     return x;
 }
 
-// Relaxed agent-scope atomics on the tail hand-off's control words (performed past the XCDs' L2s)
-__device__ __forceinline__ void add_agent(uint32_t* p, uint32_t v) {
-    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t add_agent_ret(uint32_t* p, uint32_t v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// hand-off control words (u32 index into EnvArgs::steal, each on a 128-B line of its own; the u64 at
-// index 0 is pull << 32 | push)
-enum { STEAL_BUSY = 32 };
-enum : uint64_t { STEAL_TAG_ENV = 1, STEAL_TAG_DONE = 2 };
-// minimum s_memrealtime ticks (100 MHz) between a wave's checks for pullers to hand envs to
-#ifndef PBN_STEAL_CHECK_TICKS
-#define PBN_STEAL_CHECK_TICKS 4000
-#endif
-constexpr uint64_t STEAL_CHECK_TICKS = PBN_STEAL_CHECK_TICKS;
-// a waiting puller's poll period (s_sleep units of 64 cycles: 127 = ~3.4 us) and poll bound (~60 s)
-#ifndef PBN_STEAL_POLL_SLEEP
-#define PBN_STEAL_POLL_SLEEP 127
-#endif
-constexpr uint32_t STEAL_MAX_POLLS = 1u << 24;
 
 
 template <int W, int KIND, int REPLAY, int FAST>
@@ -670,6 +649,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     } else {
         stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     }
+    // workgroup hand-off (TAIL, steal_local): control words after the draw buffers (busy waves, idle
+    // mask); each wave's mailbox flag sits in its own draw buffer's table region (cleared on going idle)
+    uint32_t* const wctl = reinterpret_cast<uint32_t*>(lds + a.off_gen + (BLOCK / 64) * ENV_GEN_WAVE_BYTES);
+    if (TAIL && a.steal_local && threadIdx.x == 0) {
+        wctl[0] = BLOCK / 64;  // busy
+        wctl[1] = 0u;          // idle mask
+    }
     __syncthreads();
     const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes + a.erec_shift) + threadIdx.x};
 #ifdef PBN_STAMPS
@@ -705,155 +691,109 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
 
-    // ---- hand-off of tail envs between waves (TAIL; EnvArgs::steal). A wave in tail mode resolves
-    // its live envs one after another; a long until-attractor loop (pbn_target_multi.py:135-146) then
-    // waits behind the others while waves that have run out of envs sit idle. Queue of slots, one per
-    // ticket: an idle wave takes a pull ticket j and waits for slot j; a tail wave holding envs it has
-    // not started on, seeing more pull tickets than published slots, claims slots with one fetch_add
-    // on the push half of the same word, writes one env per slot (lane registers + plane column) with
-    // plain stores, releases them at agent scope and tags the slot. The puller resumes the env in lane
-    // 0 -- bit-exact, since the env's Philox stream is keyed by its global id, update index and env
-    // step, not by the wave. Pushers never wait for another wave. Every read of a word another wave
-    // wrote is an atomic read-modify-write (performed past the XCDs' L2s: a plain or sc1 poll can be
-    // served from a stale L2 line for milliseconds; measured). Termination: each wave counts itself
-    // busy from its start until it holds no env; a puller leaves when no wave is busy and no slot at
-    // or past its ticket was claimed (claims are made only by busy waves), or on a DONE tag from the
-    // wave whose decrement emptied the count -- that wave first takes a ticket itself, so slots
-    // claimed past the last puller are still taken.
-    uint32_t* const sctl = TAIL && a.steal ? reinterpret_cast<uint32_t*>(a.steal) : nullptr;
-    unsigned long long* const qword = reinterpret_cast<unsigned long long*>(a.steal);  // pull << 32 | push
-    uint64_t* const slots = a.steal + STEAL_CTL_WORDS;                                   // [steal_cap][SLOT]
-    uint64_t next_check = 0;  // s_memrealtime of this wave's next allowed hand-off check
-    if (sctl && lane == 0) add_agent(&sctl[STEAL_BUSY], 1u);
-    auto rmw_ld = [](uint64_t* p) { return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto qw_add = [&](uint64_t v) { return (uint64_t)atomicAdd(qword, (unsigned long long)v); };
-    // publish the k highest lanes of cand, k <= pullers not yet served
-    auto steal_push = [&](uint64_t cand) {
-#ifdef PBN_STEAL_NOPUSH
-        return;
-#endif
+    // ---- hand-off of tail envs between the waves of a workgroup (TAIL, EnvArgs::steal_local), in LDS.
+    // A wave in tail mode resolves its live envs one after another, so a long until-attractor loop
+    // (pbn_target_multi.py:135-146) waits behind the others while sibling waves that have run out of
+    // envs sit idle. A wave that runs out of envs sets its bit in the workgroup's idle mask and waits
+    // on a flag in its own draw buffer (unused while it holds no env); a tail wave holding envs it has
+    // not started on (checked when it starts an env and every 16 blocks) claims idle waves (clearing
+    // their bits), writes one env per claimed wave (lane registers + state words) into that wave's
+    // buffer, counts the claimed wave busy and raises its flag; the claimed wave resumes the env in
+    // lane 0. Bit-exact: the env's Philox stream is keyed by its global id, update index and env step,
+    // not by the wave. A wave leaves when no wave of its workgroup is busy and it can clear its own
+    // idle bit (nobody claimed it). Tried and dropped: the same between any waves of the grid through
+    // device-memory slots -- correct, but 7-20x slower (every cross-XCD read has to be an atomic, and
+    // pushers stalled for milliseconds behind them).
+    const uint32_t wv_in_wg = threadIdx.x >> 6;
+    auto box_of = [&](uint32_t w) {
+        return reinterpret_cast<uint64_t*>(lds + a.off_gen + w * ENV_GEN_WAVE_BYTES + ENV_CHUNK * 128 + 64);
+    };
+    auto flag_of = [&](uint32_t w) {
+        return reinterpret_cast<uint32_t*>(lds + a.off_gen + w * ENV_GEN_WAVE_BYTES + ENV_CHUNK * 128);
+    };
+    auto ldl = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto local_push = [&](uint64_t cand) {
         if constexpr (TAIL) {
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (now < next_check) return;
-            next_check = now + STEAL_CHECK_TICKS;
-#ifdef PBN_STAMPS
-            est[21] += 1;
-#endif
-            uint32_t k = 0, base = 0;
+            uint32_t claimed = 0;
             if (lane == 0) {
-                // slots claimed by compare-and-swap (pushers only, each at most once per check): never
-                // past steal_push_cap, so every claimed slot is written
-                unsigned long long q = qw_add(0ull);
-                for (;;) {
-                    const uint32_t pull = (uint32_t)(q >> 32), push = (uint32_t)q;
-                    uint32_t n = pull > push ? min(pull - push, (uint32_t)__popcll(cand)) : 0u;
-                    n = push < a.steal_push_cap ? min(n, a.steal_push_cap - push) : 0u;
-                    if (n == 0u) break;
-                    const unsigned long long seen = atomicCAS(qword, q, q + n);
-                    if (seen == q) {
-                        base = push;
-                        k = n;
-                        break;
+                uint32_t idle = ldl(&wctl[1]);
+                uint32_t n = min((uint32_t)__popc(idle), (uint32_t)__popcll(cand));
+                while (idle != 0u && n != 0u) {
+                    const uint32_t w = (uint32_t)__ffs(idle) - 1u, bit = 1u << w;
+                    idle &= ~bit;
+                    if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
+                        claimed |= bit;
+                        --n;
                     }
-                    q = seen;
                 }
             }
-            k = (uint32_t)__shfl((int)k, 0);
-            if (k == 0u) return;
-            base = (uint32_t)__shfl((int)base, 0);
+            claimed = (uint32_t)__shfl((int)claimed, 0);
+            if (claimed == 0u) return;
+            const uint32_t k = (uint32_t)__popc(claimed);
             const uint32_t above = lane < 63u ? (uint32_t)__popcll(cand >> (lane + 1u)) : 0u;
             const bool mine = ((cand >> lane) & 1ull) != 0ull && above < k;
-            uint64_t* box = slots + (uint64_t)(base + above) * STEAL_SLOT_WORDS;
+            uint32_t tw = 0;  // the above-th claimed wave
             if (mine) {
-                // write-through (sc1) stores: performed at memory once drained, where the puller's
-                // atomic reads are performed -- no agent-scope release (buffer_wbl2 writes back the whole
-                // XCD L2; hundreds of pushers doing so took milliseconds each, measured)
-                auto put = [&](int k2, uint64_t v) {
-                    __hip_atomic_store(&box[k2], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                };
+                uint32_t c = claimed;
+                for (uint32_t r = 0; r < above; ++r) c &= c - 1u;
+                tw = (uint32_t)__ffs(c) - 1u;
+                uint64_t* box = box_of(tw);
                 uint64_t s[W];
                 from_plane<W>(P, s);
-                put(1, (uint64_t)e);
-                put(2, (uint64_t)nst);
-                put(3, (uint64_t)t | (uint64_t)used << 32);
-                put(4, (uint64_t)m_lo | (hit0 ? 1ull << 32 : 0ull));
-                put(5, (uint64_t)(int64_t)n_act);
+                box[0] = (uint64_t)e;
+                box[1] = (uint64_t)nst;
+                box[2] = (uint64_t)t | (uint64_t)used << 32;
+                box[3] = (uint64_t)m_lo | (hit0 ? 1ull << 32 : 0ull);
+                box[4] = (uint64_t)(int64_t)n_act;
 #pragma unroll
                 for (int k2 = 0; k2 < W; ++k2) {
-                    put(6 + k2, o0[k2]);
-                    put(6 + W + k2, s[k2]);
+                    box[5 + k2] = o0[k2];
+                    box[5 + W + k2] = s[k2];
                 }
             }
-            // the env drained before its tag, the tag drained before anything later of this wave (its
-            // busy decrement): MI355X_MICROARCH.md's write-through hand-off form, read back by atomics
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (mine) {
-                __hip_atomic_store(&box[0], (uint64_t)a.steal_seq << 32 | STEAL_TAG_ENV, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                (void)__hip_atomic_fetch_add(&wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(flag_of(tw), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 e = -1;
                 exhausted = true;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) atomicAdd(a.steal_count, k);  // diagnostics (pbn_env_handoffs)
 #ifdef PBN_STAMPS
             est[16] += k;
-            if (!est[19]) est[19] = now;
-            est[20] += __builtin_amdgcn_s_memrealtime() - now;
 #endif
         }
     };
-    // every lane idle and the work queue dry: take a pull ticket and wait for its slot (the env is
-    // resumed in lane 0: true), or leave (false)
-    auto steal_pop = [&]() -> bool {
+    auto local_pop = [&]() -> bool {
         if constexpr (TAIL) {
 #ifdef PBN_STAMPS
             const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
             if (!est[18]) est[18] = t_in;
 #endif
-            int32_t got = 0;  // 1: an env arrived; -1: leave
-            uint64_t* box = nullptr;
+            int32_t got = 0;
             if (lane == 0) {
-                const bool last = add_agent_ret(&sctl[STEAL_BUSY], 0xFFFFFFFFu) == 1u;  // no wave busy now
-                const uint64_t q = qw_add(1ull << 32);
-                const uint32_t j = (uint32_t)(q >> 32);
-                box = slots + (uint64_t)j * STEAL_SLOT_WORDS;
-                const uint64_t want = (uint64_t)a.steal_seq << 32 | STEAL_TAG_ENV;
-                if (j >= a.steal_cap) {  // never expected: tickets <= waves + envs
-                    atomicOr(a.error, 2);
-                    got = -1;
-                } else if (last && j >= (uint32_t)q) {
-                    // the last busy wave, and no slot claimed at or past its ticket: no env is left
-                    // anywhere; the pullers waiting on unclaimed slots [push, pull) are told to leave
-                    got = -1;
-                    for (uint32_t x = (uint32_t)q; x < j; ++x)
-                        __hip_atomic_store(&slots[(uint64_t)x * STEAL_SLOT_WORDS],
-                                           (uint64_t)a.steal_seq << 32 | STEAL_TAG_DONE, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    for (uint32_t n = 0;; ++n) {
-                        const uint64_t tag = rmw_ld(box);
-                        if (tag == want) {
-                            got = 1;
-                            break;
-                        }
-                        if (tag == ((uint64_t)a.steal_seq << 32 | STEAL_TAG_DONE)) {
-                            got = -1;
-                            break;
-                        }
-                        // nobody busy and no slot claimed at or past the ticket: leave (the claim, made
-                        // while busy, would be seen here: both words are read by atomics, busy first)
-                        if ((n & 15u) == 0u && add_agent_ret(&sctl[STEAL_BUSY], 0u) == 0u &&
-                            (uint32_t)qw_add(0ull) <= j) {
-                            got = -1;
-                            break;
-                        }
-                        if (n >= STEAL_MAX_POLLS) {  // never expected; leave rather than hang the GPU
-                            atomicOr(a.error, 2);
-                            got = -1;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(PBN_STEAL_POLL_SLEEP);
+                const uint32_t bit = 1u << wv_in_wg;
+                // the flag shares bytes with lane mode's draw tables: cleared before the idle bit is set
+                // (a wave's LDS operations complete in order; no pusher writes it before the bit)
+                __hip_atomic_store(flag_of(wv_in_wg), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                (void)__hip_atomic_fetch_or(&wctl[1], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                (void)__hip_atomic_fetch_add(&wctl[0], 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (;;) {
+                    if (ldl(flag_of(wv_in_wg)) != 0u) {
+                        got = 1;
+                        break;
                     }
-                    if (got == 1) add_agent(&sctl[STEAL_BUSY], 1u);
+                    if (ldl(&wctl[0]) == 0u) {
+                        // nobody busy: leave, unless a pusher claimed this wave before the count reached 0
+                        if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
+                            got = -1;
+                            break;
+                        }
+                        while (ldl(flag_of(wv_in_wg)) == 0u) __builtin_amdgcn_s_sleep(1);
+                        got = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
                 }
             }
             got = __shfl(got, 0);
@@ -862,28 +802,32 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             est[15] += got > 0 ? 1u : 0u;
 #endif
             if (got < 0) return false;
-            if (lane == 0) {  // the payload by atomic reads as well (past any stale L2 line)
-                e = (int64_t)rmw_ld(box + 1);
-                nst = (int64_t)rmw_ld(box + 2);
-                const uint64_t tu = rmw_ld(box + 3), mh = rmw_ld(box + 4);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lane == 0) {
+                const uint64_t* box = box_of(wv_in_wg);
+                e = (int64_t)box[0];
+                nst = (int64_t)box[1];
+                const uint64_t tu = box[2], mh = box[3];
                 t = (uint32_t)tu;
                 used = (uint32_t)(tu >> 32);
                 m_lo = (uint32_t)mh;
                 hit0 = ((mh >> 32) & 1ull) != 0ull;
-                n_act = (int)(int64_t)rmw_ld(box + 5);
+                n_act = (int)(int64_t)box[4];
                 uint64_t s[W];
 #pragma unroll
                 for (int k2 = 0; k2 < W; ++k2) {
-                    o0[k2] = rmw_ld(box + 6 + k2);
-                    s[k2] = rmw_ld(box + 6 + W + k2);
+                    o0[k2] = box[5 + k2];
+                    s[k2] = box[5 + W + k2];
                 }
                 to_plane<W>(P, s);
                 capped = false;
+                __hip_atomic_store(flag_of(wv_in_wg), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             return true;
         }
         return false;
     };
+
 
     // Start env step t (or the first later step whose action row is valid) of lane env e from
     // state s: flips (:120-131), observation before the update (:133), plane, counters. With no
@@ -956,7 +900,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         const uint64_t act = __ballot(e >= 0);
         if (act == 0) {
             if (__ballot(!exhausted) == 0) {
-                if (sctl && steal_pop()) continue;  // a handed-off env in lane 0
+                if (TAIL && a.steal_local && local_pop()) continue;  // a handed-off env in lane 0
                 break;
             }
             continue;
@@ -1006,7 +950,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     tmode = true;
                 }
                 // envs beyond the one resolved next go to idle waves, if there are any
-                if (sctl && (act & (act - 1ull)) != 0ull) steal_push(act & (act - 1ull));
+                if (a.steal_local && (act & (act - 1ull)) != 0ull) local_push(act & (act - 1ull));
                 const uint32_t L = (uint32_t)__ffsll((unsigned long long)act) - 1u;
                 uint32_t u = (uint32_t)__shfl((int)used, (int)L);
                 uint32_t m = (uint32_t)__shfl((int)m_lo, (int)L);
@@ -1108,9 +1052,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     D = Dn;
                     wave_sync();
                     // every 16 blocks: idle waves may have appeared since this env was started
-                    if (sctl && (++nblk & 15u) == 0u) {
+                    if (a.steal_local && (++nblk & 15u) == 0u) {
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
-                        if (others) steal_push(others);
+                        if (others) local_push(others);
                     }
                 }
                 if (lane == L) {
@@ -2020,7 +1964,8 @@ uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nod
     if (fast == 3) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
     const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
     (void)n_nodes;
-    return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES : planes;
+    // fast == 4: 16 B of workgroup hand-off control after the per-wave draw buffers
+    return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES + (fast == 4 ? 16u : 0u) : planes;
 }
 
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes) {

@@ -116,18 +116,9 @@ struct EnvArgs {
                               // 64 updates per block, once it holds at most this many (0 = never)
     uint32_t lane_limit;      // fast == 4: lanes per wave that take envs from the work queue (64 = all;
                               // <= tail_max: every wave in tail mode from its first env)
-    // fast == 4: hand-off of tail envs between waves (null = off): STEAL_CTL_WORDS u64 of control words
-    // (zeroed per launch: pull << 32 | push tickets, busy waves), then steal_cap slots of
-    // STEAL_SLOT_WORDS u64 (word 0 = tag: launch << 32 | 1 env / 2 leave; then the env)
-    uint64_t* steal;
-    uint32_t steal_cap;       // slots = pull tickets: a wave takes one each time it runs out of envs
-    uint32_t steal_push_cap;  // envs handed off per launch at most (slots claimed by pushers)
-    uint32_t steal_seq;       // this launch's tag (never 0; the slots are zeroed when allocated)
+    int32_t steal_local;      // fast == 4: hand-off of tail envs between the waves of a workgroup (LDS)
+    uint32_t* steal_count;    // envs handed off in this launch (diagnostics), zeroed per launch
 };
-
-constexpr uint32_t STEAL_CTL_WORDS = 32;   // the ticket word and the busy count, each on a 128-B line
-constexpr uint32_t STEAL_SLOT_WORDS = 32;  // 256 B (whole lines): tag, e, nst, t | used, m_lo | hit0, n_act,
-                                           // o0[W], state[W] (W <= 8)
 
 constexpr uint32_t MT_ROW = 624;
 

@@ -88,8 +88,9 @@ typedef struct {
                            wave-generated draws, 3 = group mode (k_env_grp), 4 = 2 with one counter word (<= 4 cubes) */
     int32_t env_lane_limit; /* last R6 env-step launch, env_kernel 4: lanes per wave taking envs from the work
                                queue (64 = every lane; 1 = one env per wave at a time, resolved 64 updates per block) */
-    int32_t env_handoff;    /* last R6 env-step launch, env_kernel 4: 1 if waves in tail mode could hand envs
-                               to idle waves (on with PBNSIM_ENV_STEAL=1); count: pbn_env_handoffs */
+    int32_t env_handoff;    /* last R6 env-step launch, env_kernel 4: 1 if a wave in tail mode could hand envs it had
+                               not started on to idle waves of its workgroup (PBNSIM_ENV_STEAL=0 turns it off);
+                               count: pbn_env_handoffs */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).

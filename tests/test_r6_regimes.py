@@ -258,19 +258,22 @@ def test_high_cap_matches_oracle(G, oracle_mod, spec):
     b.close()
 
 
+@pytest.mark.parametrize("steal", ["1", "0"])
 @pytest.mark.parametrize("mode", ["per_step", "fused"])
-def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, mode):
-    """Tail envs handed from wave to wave (k_env mode 4, ``EnvArgs::steal``): at the reference's
-    unbounded-loop cap (2^20) one wave's long until-attractor loops would run one after another in
-    its tail while waves whose envs all ended sit idle, so tail waves pass envs (registers + plane
-    column, through device-memory slots) to idle waves, which resume them in lane 0. 32 workgroups
-    (128 waves) hold one env per lane; the launch must hand envs off, and every env of every step
-    equals the oracle (obs, reward, flags, update counts, final state and step counters)."""
+def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, mode, steal):
+    """Tail envs handed from wave to wave (k_env mode 4, ``EnvArgs::steal_local``): at the reference's
+    unbounded-loop cap (2^20) a wave's long until-attractor loops would run one after another in its
+    tail while sibling waves whose envs all ended sit idle, so a tail wave passes envs it has not
+    started on (registers + plane column, through the idle wave's LDS draw buffer) to idle waves of its
+    workgroup, which resume them in lane 0. 32 workgroups (128 waves) hold one env per lane; with the
+    hand-off on (the default) the launches must hand envs off, with PBNSIM_ENV_STEAL=0 none; either
+    way every env of every step equals the oracle (obs, reward, flags, update counts, final state and
+    step counters)."""
     import torch
 
     monkeypatch.setenv("PBNSIM_ENV_LANES", "64")
     monkeypatch.setenv("PBNSIM_ENV_GRID", "32")
-    monkeypatch.setenv("PBNSIM_ENV_STEAL", "1")
+    monkeypatch.setenv("PBNSIM_ENV_STEAL", steal)
     import sys
     from pathlib import Path
 
@@ -311,8 +314,8 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
             handed.append(b.env_handoffs())
     info = b.info()
     assert info["env_kernel"] == 4 and info["env_lane_limit"] == 64 and info["env_grid"] == 32
-    assert info["env_handoff"] == 1
-    assert sum(handed) > 0, handed  # the hand-off path ran
+    assert info["env_handoff"] == int(steal)
+    assert (sum(handed) > 0) == (steal == "1"), handed  # the hand-off path ran (or did not)
     for t in range(T):
         ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=cap)
         obs, rew, flags, nup = got[t]

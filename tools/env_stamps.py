@@ -101,15 +101,13 @@ def main():
         res["end_us_by_capped_envs"] = {int(k): round(float(np.median(endt[ncap == k])), 1)
                                         for k in np.unique(ncap) if (ncap == k).sum() >= 8}
         res["capped_envs_per_wave"] = {q: float(np.percentile(ncap, q)) for q in (10, 50, 90, 100)}
-        # tail hand-off between waves (k_env mode 4, EnvArgs::steal): per wave envs received / pushed,
-        # time spent idle waiting in the hand-off, first idle, first push, time inside pushes
+        # tail hand-off between a workgroup's waves (k_env mode 4, EnvArgs::steal_local): per wave envs
+        # received / handed off, time spent idle waiting for one, first time idle
         pct = lambda v: {f"p{q}": round(float(np.percentile(v, q)), 1) for q in (0, 10, 50, 90, 100)}
         res["handoff"] = {"envs_received": pct(st[:, 15]), "envs_pushed": pct(st[:, 16]),
                           "total_received": int(st[:, 15].sum()), "total_pushed": int(st[:, 16].sum()),
-                          "idle_wait_us": pct(st[:, 17] / 100.0), "push_us": pct(st[:, 20] / 100.0),
-                          "push_checks": pct(st[:, 21]),
-                          "first_idle_us": pct((st[st[:, 18] > 0, 18] - t0) / 100.0) if (st[:, 18] > 0).any() else None,
-                          "first_push_us": pct((st[st[:, 19] > 0, 19] - t0) / 100.0) if (st[:, 19] > 0).any() else None}
+                          "idle_wait_us": pct(st[:, 17] / 100.0),
+                          "first_idle_us": pct((st[st[:, 18] > 0, 18] - t0) / 100.0) if (st[:, 18] > 0).any() else None}
         res["chunks_per_wave_p50"] = float(np.median(st[:, 8]))
         res["mean_active_lanes_per_chunk_p50"] = float(np.median(st[:, 9] / np.maximum(st[:, 8], 1)))
         out["reps"].append(res)
