@@ -21,6 +21,7 @@ run bench_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pr
 run trace_split 60 python tools/trace_split.py $(ls $O/prof_bench/*/bench_kernel_trace.csv $O/prof_bench/bench_kernel_trace.csv 2>/dev/null | head -n 1)
 run r6_lane_131k 200 python tools/r6_group_sweep.py 131072 1
 run r6_lane_1m 200 python tools/r6_group_sweep.py 1048576 1
-run r6_lone_lane 100 env PBNSIM_ENV_GROUP=1 python tools/r6_lone_wave.py
+run r6_lone_lane 100 env PBNSIM_ENV_GROUP=1 PBNSIM_ENV_LANES=64 python tools/r6_lone_wave.py
+run r6_lone_tail 100 env PBNSIM_ENV_GROUP=1 python tools/r6_lone_wave.py
 run valu_pmc 600 python tools/valu_pmc.py
 run pmc_traffic 600 python tools/pmc_traffic.py
