@@ -275,7 +275,8 @@ __device__ __forceinline__ uint32_t predictor_choice32(uint32_t i, uint32_t a, c
 
 __device__ __forceinline__ uint64_t predictor_record32(uint32_t i, uint32_t a, const uint8_t* lds,
                                                        const Thr32& X) {
-    return reinterpret_cast<const uint64_t*>(lds + X.rec_off)[i * X.rs + predictor_choice32(i, a, lds, X.tp4)];
+    // 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate): i < 512, rs <= 17
+    return reinterpret_cast<const uint64_t*>(lds + X.rec_off)[__umul24(i, X.rs) + predictor_choice32(i, a, lds, X.tp4)];
 }
 
 // Y = rec.tt[x_in0 x_in1 x_in2 x_self] (base.py:100-118 via the exported truth table).

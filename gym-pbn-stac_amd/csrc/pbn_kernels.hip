@@ -238,7 +238,7 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
         j1 = predictor_choice32(i1, c1, lds, X.tp4);
     }
     const uint64_t* rec = reinterpret_cast<const uint64_t*>(lds + X.rec_off);
-    const uint64_t r0 = rec[i0 * X.rs + j0], r1 = rec[i1 * X.rs + j1];
+    const uint64_t r0 = rec[__umul24(i0, X.rs) + j0], r1 = rec[__umul24(i1, X.rs) + j1];
     const PlaneT<SB> P{reinterpret_cast<uint32_t*>(lds + a.L.plane_off) + threadIdx.x};
     const bool last_dw = N > 64u * W - 32u;  // the plane's last dword holds nodes >= 64W - 32 only
     auto eval = [&](const uint64_t (&s)[W], uint32_t i, uint64_t r, uint32_t& self) {
