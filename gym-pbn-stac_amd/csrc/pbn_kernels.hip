@@ -1160,19 +1160,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // :134 the first update of an env step is tested on o0: "first" is 1 when the update
             // being settled is it (used == 1 after it; in the chunk, update 1's settle with used 0
             // at the chunk's start)
-            const uint32_t h0 = hit0 ? 1u : 0u;
-            const uint32_t f1 = (used == 0u && !a.first_tested) ? 1u : 0u;
+            // lane flags as 32-bit masks (0 / all ones): the bit operations below are single v_bitop3 /
+            // v_and, the counter step an AND with the changed-bit mask, used -= the active mask (as
+            // bools they took 16-bit selects, a compare and a select per update: 261 -> 249 VALU and
+            // 39 -> 24 SALU per 8 updates; 131,072 envs per step 1.37 -> 1.31 ms,
+            // profiles/r03_r6_settle_mask_ab.txt)
+            const uint32_t h0 = hit0 ? ~0u : 0u;
+            const uint32_t f1 = (used == 0u && !a.first_tested) ? ~0u : 0u;
+            uint32_t actm = ~0u, hitm = 0u;
             auto settle = [&](uint32_t pending, uint32_t first) {
-                m_lo += ((pfl ? pnd.x : 0u) ^ psg) - psg;
+                m_lo += ((pnd.x & pfl) ^ psg) - psg;
                 uint32_t zb = has_zero_byte(m_lo);
                 if constexpr (!ONE_WORD) {
-                    m_hi += ((pfl ? pnd.y : 0u) ^ psg) - psg;
+                    m_hi += ((pnd.y & pfl) ^ psg) - psg;
                     zb |= has_zero_byte(m_hi);
                 }
-                const uint32_t z = zb != 0u ? 1u : 0u;
-                const bool hit = act & (((z ^ (first & (z ^ h0))) & pending) != 0u);
-                hitf |= hit;
-                act = act & !hit;
+                const uint32_t z = zb != 0u ? ~0u : 0u;
+                const uint32_t hit = actm & (z ^ (first & (z ^ h0))) & pending;
+                hitm |= hit;
+                actm &= ~hit;
             };
             // the wave tests for "no lane active" once per ENV_UNROLL updates, not per update: the
             // per-update ballot + branch made every update wait for the whole previous one (the
@@ -1198,23 +1204,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 const uint32_t b1 = *reinterpret_cast<const uint32_t*>(pb + (q.x >> 16));
                 const uint32_t b2 = *reinterpret_cast<const uint32_t*>(pb + (q.y & 0xFFFFu));
                 const uint32_t self = *reinterpret_cast<const uint32_t*>(pb + (q.y >> 16));
-                settle(c != 0 ? 1u : 0u, c == 1 ? f1 : 0u);  // update c - 1 (nothing pending before the chunk's first)
+                settle(c != 0 ? ~0u : 0u, c == 1 ? f1 : 0u);  // update c - 1 (nothing pending before the chunk's first)
                 if constexpr (decltype(cap_near)::value)
-                    act = act & (c < lim);  // the update cap (pbn_target_multi.py's loop is unbounded)
+                    actm &= c < lim ? ~0u : 0u;  // the update cap (pbn_target_multi.py's loop is unbounded)
                 const uint32_t shs = q.z >> 24;
                 const uint32_t xs = __builtin_amdgcn_ubfe(self, shs, 1);
                 const uint32_t p = (__builtin_amdgcn_ubfe(b0, q.z, 1) << 3) |
                                    (__builtin_amdgcn_ubfe(b1, q.z >> 8, 1) << 2) |
                                    (__builtin_amdgcn_ubfe(b2, q.z >> 16, 1) << 1) | xs;
                 const uint32_t y = __builtin_amdgcn_ubfe(q.w, p, 1);
-                const uint32_t fl = (xs ^ y) & (act ? 1u : 0u);  // the bit changes (and is applied)
+                const uint32_t fl = (xs ^ y) & actm;  // the bit changes (and is applied)
                 *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(pb) + (q.y >> 16)) = self ^ (fl << (shs & 31u));
-                used += act ? 1u : 0u;
-                pfl = fl;
+                used -= actm;
+                pfl = 0u - fl;
                 psg = y - 1u;  // 0 (y = 1) or all ones (y = 0)
                 pnd = nd;
             }
-            if (__ballot(act) == 0) break;
+            if (__ballot(actm != 0u) == 0) break;
             }
             };
 
@@ -1222,7 +1228,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 chunk(std::true_type{});
             else
                 chunk(std::false_type{});
-            settle(1u, (used == 1u && !a.first_tested) ? 1u : 0u);  // the last update made
+            settle(~0u, (used == 1u && !a.first_tested) ? ~0u : 0u);  // the last update made
+            act = actm != 0u;
+            hitf = hitm != 0u;
             capped = !hitf && used >= a.update_cap;
             done = !act;
         } else
