@@ -313,13 +313,15 @@ __device__ __forceinline__ uint32_t table_eval_lds(const P_t& P, uint32_t i, uin
 // (w): the bit positions of in0, in1, in2, i in those dwords (one byte each). An update then reads
 // its four plane dwords with no index arithmetic. Inputs are < 512 (W <= 8), so every offset is
 // < 16 KiB.
-__device__ __forceinline__ uint4 env_record(uint64_t rec, uint32_t i) {
+// w: the truth table | the LDS byte address of node i's counter deltas (nd_off = the table's offset,
+// 8 B per node; the R6 kernel's LDS stays below 64 KiB) << 16
+__device__ __forceinline__ uint4 env_record(uint64_t rec, uint32_t i, uint32_t nd_off) {
     const uint32_t x0 = (uint32_t)rec & 0xFFFFu, x1 = (uint32_t)(rec >> 16) & 0xFFFFu,
                    x2 = (uint32_t)(rec >> 32) & 0xFFFFu;
     auto off = [](uint32_t x) { return (x >> 5) * (uint32_t)(BLOCK * 4); };
     return make_uint4(off(x0) | (off(x1) << 16), off(x2) | (off(i) << 16),
                       (x0 & 31u) | ((x1 & 31u) << 8) | ((x2 & 31u) << 16) | ((i & 31u) << 24),
-                      (uint32_t)(rec >> 48) | (i << 16));
+                      (uint32_t)(rec >> 48) | ((nd_off + 8u * i) << 16));
 }
 
 // Async update of node i in place on the plane; returns 1 if the bit changed.

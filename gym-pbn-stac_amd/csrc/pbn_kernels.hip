@@ -644,7 +644,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 src = 0;
                 for (uint32_t p = 0; p < tp; ++p) src += (u32_threshold(gthr[i * tp + p]) >> 32) ? 0u : 1u;
             }
-            erec[r] = env_record(src < a.L.pmax ? grec[i * a.L.pmax + src] : 0ull, i);
+            erec[r] = env_record(src < a.L.pmax ? grec[i * a.L.pmax + src] : 0ull, i, a.off_ndelta);
         }
     } else {
         stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
@@ -1143,7 +1143,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             const uint32_t lim = a.update_cap > used ? a.update_cap - used : 0u;  // updates left
             uint4 q0 = erec[gbuf[lane]];
             uint4 q1 = erec[gbuf[64 + lane]];
-            uint2 n0 = ndelta[q0.w >> 16];
+            // the node's counter deltas at the LDS address the record carries (no index arithmetic)
+            auto nd_at = [&](const uint4& q) { return *reinterpret_cast<const uint2*>(lds + (q.w >> 16)); };
+            uint2 n0 = nd_at(q0);
             uint32_t e2 = gbuf[128 + lane];
             static_assert(ENV_CHUNK >= 3 && ENV_CHUNK % ENV_UNROLL == 0, "prefetch depth / unroll");
             // Update c's counter update and attractor test are made after update c + 1's plane
@@ -1195,7 +1197,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 const uint4 q = q0;
                 const uint2 nd = n0;
                 // unconditional (clamped) prefetches: no branch, so no wait before the plane reads
-                n0 = ndelta[q1.w >> 16];
+                n0 = nd_at(q1);
                 q0 = q1;
                 q1 = erec[e2];
                 e2 = gbuf[min(c + 3, ENV_CHUNK - 1) * 64 + lane];
