@@ -1178,9 +1178,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     zb |= has_zero_byte(m_hi);
                 }
                 const uint32_t z = zb != 0u ? ~0u : 0u;
-                const uint32_t hit = actm & (z ^ (first & (z ^ h0))) & pending;
-                hitm |= hit;
-                actm &= ~hit;
+                const uint32_t t = (z ^ (first & (z ^ h0))) & pending;  // the test's outcome (o0's on :134)
+                hitm |= actm & t;  // one v_bitop3 each: no separate hit mask
+                actm &= ~t;
             };
             // the wave tests for "no lane active" once per ENV_UNROLL updates, not per update: the
             // per-update ballot + branch made every update wait for the whole previous one (the
