@@ -22,11 +22,16 @@ falling to about 9 % after ~1,000 launches -- not a clock ramp. 
 bytes follow the window actually timed: the changed fraction over exactly the K timed launches
 is measured on a twin batch (same seed: identical Philox trajectory) after the timing, and so is the
 kernel time (a HIP-event region over the same K launches of a twin batch: the timed window itself
-carries no instrumentation). The 1M line's state stays in the Infinity Cache (MALL); its peak is
-the measured ceiling of its access pattern (``tools/mall_probe.hip``: the same launch shape and
-bytes, no compute), so ``frac`` = kernel floor / kernel time; the guide's MALL gather rate stays
-beside it as a labelled, read-only reference. The HBM roofline (8 TB/s spec) comes from the 8M-env
-run (256 MiB of state).
+carries no instrumentation). ``peak`` is the fixed 8 TB/s HBM spec; the 1M line's state stays in
+the Infinity Cache (MALL), so the measured ceiling of its access pattern (``tools/mall_probe.hip``:
+the same launch shape and bytes, no compute) is reported beside it (``floor_GBs``,
+``frac_of_floor`` = kernel floor / kernel time); the guide's MALL gather rate stays as a labelled,
+read-only reference. The 8M-env run (256 MiB of state, past the MALL) carries the HBM-bound figure.
+
+Self-checks (any N): ``shard_check`` re-runs sampled global env ids as 2-env batches and compares
+them with the sharded run (Philox keyed by global id: a one-GPU run gives those ids the same
+trajectory), digesting every rank's rows in global-id order; ``dist`` names the process group's
+backend and size and every rank's kernel time; config 5's actions are keyed by global env id.
 
 Prints ONE JSON line (rank 0) with ``roofline`` and ``cpu_baseline`` (the oracle's C
 restatement on host cores, rank 0 at N = 1 only).
@@ -353,14 +358,19 @@ def valu_roofline(v, s, updates):
             "source": v.get("source", "profiles/r03_valu_pmc.json")}
 
 
-def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather=True):
+def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather=True, check=False):
     """One config-5 figure: the multi-flip until-attractor env (pbn_target_multi.py:119-154) on
     Bittner-200, ``--r6-batch`` envs per GPU (131,072: 1M over 8 GPUs), T = horizon = 100 env steps per
     chunk written to a device chunk and all-gathered across ranks (RCCL) while the next chunk runs;
-    A = 4 action slots (0 w.p. 0.75); attractors ``spec`` (r6_attractors); update cap ``cap``. Timed
-    twice: one launch per env step (closed loop), then one launch per chunk (actions known for it)."""
+    A = 4 action slots (0 w.p. 0.75) drawn by ``actions.env_actions`` from Philox seed 0xAC7 keyed by
+    GLOBAL env id and env step (SURVEY §8(d)), so the global batch is one workload at any GPU count;
+    attractors ``spec`` (r6_attractors); update cap ``cap``. Timed twice: one launch per env step
+    (closed loop), then one launch per chunk (actions known for it). Every timed chunk reports its
+    kernel time (HIP events), the slowest env's updates and (fused) the tail hand-offs of its launch;
+    with ``check`` the fused run's last chunk is checked on sampled global ids (r6_shard_check)."""
     import torch
 
+    from gym_pbn_amd.actions import env_actions
     from gym_pbn_amd.batch import EnvConfig, Net, PBNBatch
     from gym_pbn_amd.network import load_network
     from gym_pbn_amd.rollout import TrajectoryCollector, gather_chunk
@@ -372,10 +382,7 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
     cfg = EnvConfig(net, atts, horizon=T)
     sh = shard_for(rank, world, B)
     dev = _dev(device)
-    g = torch.Generator(device=dev)
-    g.manual_seed(0xAC7 + rank)
-    v = torch.randint(1, net.n_nodes + 1, (T, B, A), device=dev, generator=g, dtype=torch.int32)
-    acts = (v * (torch.rand((T, B, A), device=dev, generator=g) >= 0.75)).to(torch.int32).contiguous()
+    acts = env_actions(T, sh.env_base, B, A, net.n_nodes, seed=0xAC7, device=dev)
 
     def chunk_stats(buf):
         # per env step: the slowest env (a per-step launch waits for it) and the mean; capped envs
@@ -388,7 +395,7 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
         b = PBNBatch(net, B, device=device, env_id_base=sh.env_base, seed=0xAC7)
         col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=cap, dist=dist if gather else None, fused=fused)
 
-        def chunks():
+        def chunks(diag=None):
             ups = torch.zeros((), dtype=torch.int64, device=dev)
             stats = []
             for _ in range(n_chunks):
@@ -396,6 +403,14 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
                 u, st = chunk_stats(buf)
                 ups += u
                 stats.append(st)
+                if diag is not None:  # the collector synced the batch stream after the chunk
+                    kms_c, nl = b.timing_read()  # this chunk's launches (HIP events), then reset
+                    d = {"kernel_ms": kms_c, "launches": nl,
+                         # the env whose T env steps took the most updates: a fused chunk ends with it
+                         "slowest_env_updates": int(buf["n_updates"].to(torch.int64).sum(dim=0).max().item())}
+                    if fused:
+                        d["handoffs"] = b.env_handoffs()  # tail envs passed between the waves of a workgroup
+                    diag.append(d)
             return buf, ups, stats
 
         # warm-up: the timed loop itself, untimed, with the per-launch events on -- the first use
@@ -409,15 +424,16 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
         if dist is not None:
             dist.barrier()
         b.timing(1)  # an event pair around every launch on the batch stream: kernel time alone
+        diag = []
         t0 = time.perf_counter()
-        buf, ups, stats = chunks()
+        buf, ups, stats = chunks(diag)
         col.finish()
         _sync()
         if dist is not None:
             dist.barrier()
         dt = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
-        kms, _ = b.timing_read()
         b.timing(0)
+        kms = sum(d["kernel_ms"] for d in diag)
         local_ups = float(ups.item())
         if dist is not None:
             dist.all_reduce(ups)
@@ -425,13 +441,13 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
         tail = {"capped_frac": float(st[2].mean()), "mean_updates_per_env_step": float(st[1].mean()),
                 "max_updates_per_env_step_mean_over_steps": float(st[0].mean()),
                 "steps_whose_slowest_env_hit_the_cap": float((st[0] >= cap).mean())}
-        return b, buf, dt, float(ups.item()), tail, (kms / 1e3, local_ups)
+        return b, buf, dt, float(ups.item()), tail, (kms / 1e3, local_ups), diag
 
     # closed-loop shape first (one launch per env step, as an agent in the loop needs), then the
     # open-loop collector (actions known for the chunk: one launch walks each env through T steps)
-    b, buf, dt_step, ups_step, tail_step, k_step = run(False)
+    b, buf, dt_step, ups_step, tail_step, k_step, diag_step = run(False)
     b.close()
-    b, buf, dt, ups, tail, k_fused = run(True)
+    b, buf, dt, ups, tail, k_fused, diag = run(True)
     lanes = b.info()["env_lanes"]
     out = {"unit": "env-steps/s", "attractors": spec, "attractors_desc": desc, "update_cap": cap,
            "value": world * B * T * n_chunks / dt, "node_updates_per_s": ups / dt,
@@ -439,14 +455,18 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
            "value_one_launch_per_env_step": world * B * T * n_chunks / dt_step,
            "node_updates_per_s_one_launch_per_env_step": ups_step / dt_step,
            "batch_per_gpu": B, "global_batch": world * B, "T": T, "A": A, "env_lanes": lanes,
+           "actions": "actions.env_actions: Philox seed 0xAC7 keyed by global env id and env step (stream 9)",
            "chunks": n_chunks, "s_per_chunk": dt / n_chunks, "tail": tail,
            "tail_one_launch_per_env_step": tail_step,
+           "chunk_diag": diag, "chunk_diag_one_launch_per_env_step": diag_step,
            "chunk_bytes_per_gpu": sum(t.numel() * t.element_size() for t in buf.values())}
     for key, (ks, nu), name in ((f"k_env:bittner199:{B}:fused{T}", k_fused, "roofline"),
                                 (f"k_env:bittner199:{B}:per_step", k_step, "roofline_one_launch_per_env_step")):
         vr = (valu or {}).get(key) if (spec == "fixture" and cap == 4096) else None
         if vr and ks > 0:  # this rank's env kernels: node updates / summed kernel time (HIP events)
             out[name] = valu_roofline(vr, ks, nu)
+    if check:
+        out["shard_check"] = guarded(r6_shard_check, net, cfg, buf, sh, T, A, cap, 2 * n_chunks, device, dist)
     if dist is not None and gather:  # the gather alone: bytes received per GPU / time
         _sync()
         dist.barrier()
@@ -460,6 +480,75 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
     return out
 
 
+def r6_shard_check(net, cfg, buf, sh, T, A, cap, n_chunks_run, device, dist, n_samples=16):
+    """Config 5 at any N checks itself: for the sampled global env ids (shard.sampled_env_ids) in this
+    rank's shard, a 2-env batch with the same global ids, seed, actions (keyed by global id), cap and
+    chunk sequence -- what a one-GPU run gives those envs -- must reproduce the last chunk's obs,
+    reward, flags and update counts bit for bit; rank 0 digests every rank's rows in global-id order."""
+    import numpy as np
+    import torch
+
+    from gym_pbn_amd.actions import env_actions
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.rollout import FIELDS, TrajectoryCollector
+    from gym_pbn_amd.shard import gather_rows, max_over_ranks, rows_digest, sampled_env_ids
+
+    dev = _dev(device)
+    rows, bad = [], 0
+    for g in sampled_env_ids(sh.n_global, n_samples):
+        if not sh.env_base <= g < sh.env_base + sh.n_local - 1:
+            continue
+        s = PBNBatch(net, 2, device=device, env_id_base=g, seed=0xAC7)
+        col = TrajectoryCollector(s, cfg, T, A, dev, update_cap=cap, dist=None, fused=True)
+        a2 = env_actions(T, g, 2, A, net.n_nodes, seed=0xAC7, device=dev)
+        for _ in range(n_chunks_run):
+            sbuf, _ = col.step_chunk(a2)
+        col.finish()
+        j = g - sh.env_base
+        ref = {k: buf[k][:, j:j + 2].contiguous() for k in FIELDS}
+        bad += 0 if all(torch.equal(sbuf[k], ref[k]) for k in FIELDS) else 1
+        rows.append((g, b"".join(np.ascontiguousarray(ref[k].cpu().numpy()).tobytes() for k in FIELDS)))
+        s.close()
+    all_rows = gather_rows(rows, dist)
+    bad = max_over_ranks(float(bad), dist, device=dev)
+    return {"sampled_env_pairs": len(all_rows), "match": bad == 0, "digest": rows_digest(all_rows),
+            "ranks": dist.get_world_size() if dist is not None else 1,
+            "method": "per rank, the sampled global ids in its shard re-run as 2-env batches (same ids, seed, "
+                      "actions, cap, chunk sequence); last chunk's obs/reward/flags/n_updates compared bit for bit; "
+                      "digest = blake2b-64 over every rank's rows in global-id order (shard.rows_digest)"}
+
+
+def step_shard_check(net, state, device, seed, env_base, n_local, n_global, n_launches, dist, n_samples=32):
+    """The headline at any N checks itself: for the sampled global env ids in this rank's shard, a
+    2-env batch with the same global ids and seed, randomized and stepped the same number of launches
+    (what a one-GPU run gives those ids: Philox keyed by global id), must equal the sharded batch's
+    final state; rank 0 digests every rank's rows in global-id order."""
+    import numpy as np
+
+    from gym_pbn_amd.batch import PBNBatch
+    from gym_pbn_amd.shard import gather_rows, max_over_ranks, rows_digest, sampled_env_ids
+
+    rows, bad = [], 0
+    for g in sampled_env_ids(n_global, n_samples):
+        if not env_base <= g < env_base + n_local - 1:
+            continue
+        s = PBNBatch(net, 2, device=device, env_id_base=g, seed=seed)
+        s.randomize()
+        s.step(n_launches)
+        mine = s.get_state()
+        s.close()
+        ref = np.ascontiguousarray(state[g - env_base:g - env_base + 2])
+        bad += 0 if np.array_equal(mine, ref) else 1
+        rows.append((g, ref.tobytes()))
+    all_rows = gather_rows(rows, dist)
+    bad = max_over_ranks(float(bad), dist, device=_dev(device))
+    return {"sampled_env_pairs": len(all_rows), "match": bad == 0, "digest": rows_digest(all_rows),
+            "ranks": dist.get_world_size() if dist is not None else 1,
+            "method": "per rank, the sampled global ids in its shard re-run as 2-env batches (same ids and seed, "
+                      "randomize + the same launches); final states compared bit for bit; digest = blake2b-64 over "
+                      "every rank's rows in global-id order (shard.rows_digest)"}
+
+
 R6_HIGH_CAP = 1 << 20  # the longest loop measured at config 5 ran 78,057 updates (profiles/r03_r6_cap_sweep.json)
 
 
@@ -469,7 +558,7 @@ def r6_supplement(args, world, rank, device, dist, valu):
     the loop never reached in measurement (so comparable to the reference's unbounded loop,
     pbn_target_multi.py:135-146): the same attractors, and SURVEY §8(d)'s attractor spec."""
     out = {"metric": "R6 env-steps/s (whole node) incl. per-chunk trajectory all-gather",
-           **r6_figure(args, world, rank, device, dist, valu, "fixture", 4096, args.r6_chunks)}
+           **r6_figure(args, world, rank, device, dist, valu, "fixture", 4096, args.r6_chunks, check=True)}
     if args.r6_variants:
         out["high_cap"] = guarded(r6_figure, args, world, rank, device, dist, valu, "fixture", R6_HIGH_CAP, 1)
         out["spec_attractors"] = guarded(r6_figure, args, world, rank, device, dist, valu, "spec", R6_HIGH_CAP, 1)
@@ -501,6 +590,37 @@ def r6_attractors(spec, n_nodes):
                   "attractors (get_attractors_from_cabean.py:57-81), other bits '*'")
 
 
+def per_rank(values: dict, dist):
+    """Every rank's ``values`` on every rank (rank order), e.g. per-rank kernel time at N > 1."""
+    if dist is None:
+        return [values]
+    parts = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, values)
+    return parts
+
+
+def process_census():
+    """This process's live child processes (recursive) and thread count when the line is printed, and
+    again at exit on stderr -- to name whatever the driver counts after the run (BENCH procs_at_end)."""
+    try:
+        import psutil
+
+        me = psutil.Process()
+        kids = []
+        for c in me.children(recursive=True):
+            try:
+                kids.append({"pid": c.pid, "name": c.name(), "cmdline": " ".join(c.cmdline())[:160]})
+            except psutil.Error:
+                kids.append({"pid": c.pid, "name": "?"})
+        return {"children": kids, "threads": me.num_threads()}
+    except Exception as exc:  # diagnostics only
+        return {"error": f"{type(exc).__name__}: {exc}"}
+
+
+def _census_at_exit():
+    print("bench.py exit census: " + json.dumps(process_census()), file=sys.stderr, flush=True)
+
+
 def guarded(fn, *a):
     try:
         return fn(*a)
@@ -510,6 +630,9 @@ def guarded(fn, *a):
 
 def main():
     args = parse()
+    import atexit
+
+    atexit.register(_census_at_exit)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local = dist_env()
@@ -599,6 +722,7 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = max_over_ranks(t1 - t0, dist, device=_dev(device))
+    final_state = batch.get_state()  # host copy for the shard self-check below (after the window)
     batch.close()
     # kernel time of the same window: a twin batch (same network, seed and env ids: the identical
     # Philox trajectory, so the same envs change and are written back per launch) runs the same W
@@ -613,8 +737,8 @@ def main():
     twin.step(args.steps)
     twin.timing(0)
     _sync()
-    kernel_ms, launches = twin.timing_read()
-    kernel_ms = max_over_ranks(kernel_ms, dist, device=_dev(device))
+    local_kernel_ms, launches = twin.timing_read()
+    kernel_ms = max_over_ranks(local_kernel_ms, dist, device=_dev(device))
     twin.close()
 
     # the bytes the timed launches had to move: the fraction of envs written back per launch over
@@ -622,6 +746,12 @@ def main():
     # clock state (32 B read per env, the changed envs' 32 B written back, no compute)
     q = window_changed_fraction(net, B, device, args.seed, shard.env_base, args.warmup, args.steps) \
         if rank == 0 else None
+    # sharded-run self-check (every rank; collectives inside): sampled global ids re-run on their own
+    check = guarded(step_shard_check, net, final_state, device, args.seed, shard.env_base, B, world * B,
+                    args.warmup + args.steps, dist)
+    del final_state
+    ranks = per_rank({"rank": rank, "kernel_us": local_kernel_ms * 1e3 / max(launches, 1),
+                      "elapsed_s": t1 - t0, "device": device}, dist)
     floor_us = None
     if floor is not None and q is not None:
         try:
@@ -640,13 +770,12 @@ def main():
         achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
         kernel_us = avg_kernel_s * 1e6 if launches else None
         floor_GBs = alg_bytes / (floor_us / 1e6) / 1e9 if floor_us else None
-        peak = floor_GBs if floor_GBs else MALL_PEAK_GBS
         rf = {
-            "bound": "mall",
+            "bound": "hbm",
             "achieved": achieved,
-            "peak": peak,
+            "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": (achieved / peak) if achieved else None,
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
             "kernel": f"pbn::k_step<{W},1,1,0,1024> (predictor mix, dirty store, Philox, 1024-thread groups)",
             "alg_bytes_per_launch": alg_bytes,
@@ -658,11 +787,13 @@ def main():
                       "trajectory) right after the timed window; the timed window itself carries no events",
             "residency": "the 32 MiB state stays in the 256 MiB Infinity Cache (MALL) and the XCDs' L2 between "
                          "launches; the HBM-bound figure is hbm_8m",
-            "peak_source": ("measured ceiling of this access pattern: alg_bytes_per_launch / floor_us, the live "
-                            "no-compute probe tools/mall_probe.hip (frac = frac_of_floor)") if floor_GBs else
-                           "probe unavailable: MI355X_MICROARCH.md Indexed rows gather rate (read-only)",
+            "peak_source": "MI355X HBM3E spec, 8 TB/s (MI355X_MICROARCH.md): a fixed hardware ceiling; the 32 MiB "
+                           "state is MALL-resident, and the measured ceiling of this access pattern is floor_GBs",
             "floor_us": floor_us,
+            "floor_GBs": floor_GBs,
             "frac_of_floor": (floor_us / kernel_us) if (floor_us and kernel_us) else None,
+            "frac_of_floor_note": "kernel floor / kernel time: the probe-relative figure (changes with the probe's "
+                                  "run); frac is against the fixed 8 TB/s spec",
             "floor_source": "tools/mall_probe.hip run live after the timed launches: the same launch shape "
                             "(1024-thread groups, 2 per CU, env pairs), 32 B read per env, changed_env_frac of the "
                             "envs (drawn afresh per launch) written back, no compute",
@@ -711,11 +842,15 @@ def main():
             },
             "roofline": rf,
             "node_updates_per_s": value,
+            "dist": {"backend": dist.get_backend() if dist is not None else None,
+                     "world_size": dist.get_world_size() if dist is not None else 1, "per_rank": ranks},
+            "shard_check": check,
             "order": "supplements (rollout, config 2, 8M past-MALL, config 5) ran before the headline",
             **sup,
         }
         if world == 1 and not args.no_cpu_baseline:  # the host-core baseline: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(net, args.cpu_seconds)
+        out["process_census"] = process_census()
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

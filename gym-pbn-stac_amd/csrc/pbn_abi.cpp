@@ -1333,11 +1333,11 @@ int pbn_get_n_steps(pbn_batch* b, int64_t* n_steps) {
 // Per-step call, Bittner-200, 1 MI355X (256 CUs): G = 8 beats lane mode up to 32k envs (0.21 vs
 // 0.33 ms at B = 1, 0.88 vs 1.99 ms at 8k, 1.85 vs 2.04 ms at 32k) and loses from 64k on (2.31 vs
 // 2.07 ms; 131k: 3.28 vs 2.60 ms) -- the crossover sits near 48k envs.
-// Group mode (G = 8 lanes per env) for small batches -- except with <= 4 cubes, where the lane
-// kernel's tail mode with one env per wave (env_lane_limit) is faster at every batch size measured
-// (profiles/r03_r6_lanes_sweep.json)
-static int env_group_size(const pbn_batch* b, int n_cubes) {
-    if (n_cubes <= 4) return 1;
+// Group mode (G = 8 lanes per env) for small batches -- except where the tail kernel (k_env mode 4:
+// <= 4 cubes and its 16-B env records fit) applies: its tail mode with one env per wave
+// (env_lane_limit) is faster at every batch size measured (profiles/r03_r6_lanes_sweep.json)
+static int env_group_size(const pbn_batch* b, bool tail_kernel) {
+    if (tail_kernel) return 1;
     return b->B * 8 <= (uint64_t)b->n_cu * 1536 ? 8 : 1;
 }
 
@@ -1351,28 +1351,32 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
                 b->net->N <= 512 && !b->env_no_gen)
                    ? 2
                    : cfg->fast;
-    // group mode (k_env_grp: G lanes per env, G updates per round trip)
-    int grp = 1;
-    if (mode == 2 && b->net->N <= 256) {
-        grp = b->env_group ? b->env_group : env_group_size(b, cfg->H);
-        if (grp != 2 && grp != 4 && grp != 8) grp = 1;
-        if (grp > 1) mode = 3;
-    }
     // cooperative-draw mode keeps 16-B env records in LDS where the 8-B predictor records were
-    // (pbn_device.hpp env_record): the tables after them move up by erec_shift
+    // (pbn_device.hpp env_record): the tables after them move up by erec_shift. Whether they fit is
+    // decided first, so that the group-size rule below knows whether the tail kernel (mode 4) applies
     uint32_t erec_shift = 0;
+    bool erec_fits = false;
     if (mode == 2) {
         // rows of rs records (thr32_layout: tp4 + 1 slots at least, for the saturated choice)
         const uint32_t tp4 = (cfg->L.tp + 3u) & ~3u;
         const uint32_t nrec = (uint32_t)b->net->N * std::max(tp4 + 1u, cfg->L.pmax);
         erec_shift = cfg->L.off_rec + 16u * nrec - cfg->off_cubes;
-        if (nrec > 65535u || env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1) > 64u * 1024u) {
-            mode = cfg->fast;  // too large for the u16 record index / one workgroup's LDS
-            erec_shift = 0;
-        } else if (cfg->H <= 4) {
-            mode = 4;  // the same kernel with one packed counter word (<= 4 cubes)
-        }
+        erec_fits = nrec <= 65535u && env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1) <= 64u * 1024u;
     }
+    // group mode (k_env_grp: G lanes per env, G updates per round trip; its rows need no env records)
+    int grp = 1;
+    if (mode == 2 && b->net->N <= 256) {
+        grp = b->env_group ? b->env_group : env_group_size(b, erec_fits && cfg->H <= 4);
+        if (grp != 2 && grp != 4 && grp != 8) grp = 1;
+        if (grp > 1) mode = 3;
+    }
+    if (mode == 2) {
+        if (!erec_fits)
+            mode = cfg->fast;  // too large for the u16 record index / one workgroup's LDS
+        else if (cfg->H <= 4)
+            mode = 4;  // the same kernel with one packed counter word (<= 4 cubes)
+    }
+    if (mode != 2 && mode != 4) erec_shift = 0;
     int bpc = 1;
     if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc, b->net->N))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));

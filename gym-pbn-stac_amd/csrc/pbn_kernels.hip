@@ -29,7 +29,7 @@ namespace pbn {
 // of the step kernel's phases, kept in registers and written once at the end of the wave.
 __device__ uint64_t g_stamps[16384 * 8];
 // k_env (cooperative-draw path): per wave, ENV_STAMPS words (tools/env_stamps.py reads them)
-constexpr int ENV_STAMPS = 24;
+constexpr int ENV_STAMPS = 32;
 __device__ uint64_t g_env_stamps[16384 * ENV_STAMPS];
 #endif
 
@@ -274,11 +274,10 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
 // path's code shapes the other's register allocation and schedule (sharing one kernel cost
 // the step path 0.6 us per launch at 1M envs).
 template <int W, int KIND, int STORE, int REPLAY, int SB>
-// 1024-thread groups, W <= 4: two workgroups per CU = 8 waves per SIMD, so at most 64 VGPRs
+// 1024-thread groups, W <= 4: two workgroups per CU = 8 waves per SIMD, so at most 64 VGPRs (every
+// instance this bound applies to -- both kinds, both store modes, Philox only: SB = 1024 is never
+// launched in replay mode -- compiles without scratch, `make asm`; the stamps build keeps the bound)
 __global__ __launch_bounds__(SB, (SB == 1024 && W <= 4) ? 8 : 1)
-#ifdef PBN_STAMPS
-__attribute__((amdgpu_waves_per_eu(8, 8)))  // the product's occupancy (64 VGPRs) despite the stamps
-#endif
 void k_step(StepArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     const uint64_t stride = (uint64_t)gridDim.x * SB;
@@ -605,6 +604,13 @@ __device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
 
 
 
+// A wave's draw buffer (ENV_GEN_WAVE_BYTES) in tail mode: the per-node 64-bit writer masks from byte
+// 0 (N <= 512 nodes: 4 KiB), the hand-off flag at ENV_CHUNK * 128 and the hand-off box (5 + 2W words)
+// 64 B after it; lane mode's draw table [ENV_CHUNK][64] u16 and rank / counter tables use the same bytes
+static_assert(8u * 512u <= ENV_CHUNK * 128u, "tail writer masks (N <= 512) overlap the hand-off flag");
+static_assert(ENV_CHUNK * 128u + 64u + 8u * (5u + 2u * 8u) <= ENV_GEN_WAVE_BYTES,
+              "the hand-off box (W <= 8) overflows the wave's draw buffer");
+
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_env(EnvArgs a) {
     constexpr bool GEN = FAST == 2 || FAST == 4;
@@ -773,10 +779,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             int32_t got = 0;
             if (lane == 0) {
                 const uint32_t bit = 1u << wv_in_wg;
-                // the flag shares bytes with lane mode's draw tables: cleared before the idle bit is set
-                // (a wave's LDS operations complete in order; no pusher writes it before the bit)
+                // the flag shares bytes with lane mode's draw tables: cleared before the idle bit is set,
+                // and the bit set with release semantics, so a pusher that claims the bit (its fetch_and
+                // reads it) cannot be ordered before the cleared flag
                 __hip_atomic_store(flag_of(wv_in_wg), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                (void)__hip_atomic_fetch_or(&wctl[1], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                (void)__hip_atomic_fetch_or(&wctl[1], bit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 (void)__hip_atomic_fetch_add(&wctl[0], 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 for (;;) {
                     if (ldl(flag_of(wv_in_wg)) != 0u) {
@@ -1004,6 +1011,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 uint32_t nblk = 0;
                 TailDraw D = prepare(u);
                 while (!fin) {
+#ifdef PBN_STAMPS
+                    // tail block phases (shader clocks, s_memtime): 19 blocks, 20 cycles per block, 21 fixed-point
+                    // rounds, 22 cycles of the resolution (fixed point), 23 cycles from the block's top to the
+                    // next block's draws prepared, 24..31 blocks by rounds (0..6, 7+)
+                    const uint64_t c_top = __builtin_amdgcn_s_memtime();
+                    uint32_t nround = 0;
+#endif
                     const uint4 q = D.q;
                     const uint32_t U = u + lane;
                     const uint32_t o0 = q.x & 0xFFFFu, o1 = q.x >> 16, o2 = q.y & 0xFFFFu, os = q.y >> 16;
@@ -1014,12 +1028,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint32_t b2 = *reinterpret_cast<const uint32_t*>(colb + o2);
                     const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + os);
                     const TailDraw Dn = prepare(u + 64u);  // while those reads are in flight
+#ifdef PBN_STAMPS
+                    const uint64_t c_prep = __builtin_amdgcn_s_memtime();
+#endif
                     const uint32_t v0 = __builtin_amdgcn_ubfe(b0, q.z, 1), v1 = __builtin_amdgcn_ubfe(b1, q.z >> 8, 1),
                                    v2 = __builtin_amdgcn_ubfe(b2, q.z >> 16, 1), v3 = __builtin_amdgcn_ubfe(b3, ss, 1);
                     uint32_t x3 = v3;
                     uint32_t y = __builtin_amdgcn_ubfe(q.w, (v0 << 3) | (v1 << 2) | (v2 << 1) | v3, 1);
                     if (__ballot(D.r0 >= 0 || D.r1 >= 0 || D.r2 >= 0 || D.r3 >= 0) != 0) {
                         for (;;) {
+#ifdef PBN_STAMPS
+                            ++nround;
+#endif
                             const uint64_t Y = __ballot(y != 0u);
                             auto pick = [&](int32_t r, uint32_t v) { return r >= 0 ? (uint32_t)(Y >> r) & 1u : v; };
                             x3 = pick(D.r3, v3);
@@ -1029,6 +1049,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                             y = yn;
                         }
                     }
+#ifdef PBN_STAMPS
+                    const uint64_t c_fp = __builtin_amdgcn_s_memtime();
+#endif
                     // packed counter deltas (+ d for 0 -> 1, - d for 1 -> 0), prefix over the block
                     const uint32_t sg = y - 1u;
                     const uint32_t mk = m + wave_inclusive_add((((y ^ x3) ? D.nd : 0u) ^ sg) - sg);
@@ -1051,6 +1074,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     fin = hitf || u >= a.update_cap;
                     D = Dn;
                     wave_sync();
+#ifdef PBN_STAMPS
+                    {
+                        const uint64_t c_end = __builtin_amdgcn_s_memtime();
+                        est[19] += 1;
+                        est[20] += c_end - c_top;
+                        est[21] += nround;
+                        est[22] += c_fp - c_prep;
+                        est[23] += c_prep - c_top;
+                        est[24 + min(nround, 7u)] += 1;
+                    }
+#endif
                     // every 16 blocks: idle waves may have appeared since this env was started
                     if (a.steal_local && (++nblk & 15u) == 0u) {
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);

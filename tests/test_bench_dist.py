@@ -51,6 +51,11 @@ class _FakeBatch:
     def info(self):
         return {"env_lanes": 1, "roll_lanes": 1}
 
+    def get_state(self):
+        import numpy as np
+
+        return np.zeros((self.n_envs, self.n_words), dtype=np.uint64)
+
 
 class _FakeNet:
     def __init__(self, net):
@@ -128,6 +133,14 @@ def test_two_rank_bench_bookkeeping_on_cpu(tmp_path):
     assert "all_gather_GBs_per_gpu" in r6
     assert r6["high_cap"]["attractors"] == "fixture" and r6["high_cap"]["update_cap"] > 4096
     assert r6["spec_attractors"]["attractors"] == "spec" and r6["spec_attractors"]["update_cap"] > 4096
+    # the N > 1 line names its process group and checks its shards itself
+    assert d["dist"]["backend"] == "gloo" and d["dist"]["world_size"] == 2
+    assert [p["rank"] for p in d["dist"]["per_rank"]] == [0, 1]
+    sc = d["shard_check"]
+    assert sc["ranks"] == 2 and sc["match"] is True and sc["sampled_env_pairs"] == 32
+    assert r6["shard_check"]["ranks"] == 2 and r6["shard_check"]["sampled_env_pairs"] == 16
+    assert len(r6["chunk_diag"]) == 2 and "handoffs" in r6["chunk_diag"][0]
+    assert "process_census" in d
 
 
 def test_failed_process_group_exits_nonzero_promptly():

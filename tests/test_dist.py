@@ -117,3 +117,60 @@ def test_trajectory_chunk_gather_is_rank_major(tmp_path):
         loc = torch.load(tmp_path / f"local{r}.pt", weights_only=True)
         for k, v in loc.items():
             assert got[k].dtype == v.dtype and torch.equal(got[k][r], v), k
+
+
+def _digest_worker(rank, world, port, n_global, T, out_dir):
+    """bench.py's N > 1 self-check on CPU: rank r steps its shard (oracle = the kernels' Philox
+    stream), re-runs the sampled global ids in its shard as 2-env batches (the bench's check, with the
+    oracle in place of the GPU), digests every rank's rows in global-id order, and draws config 5's
+    actions for its shard (actions.env_actions, keyed by global env id)."""
+    sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from gym_pbn_amd.actions import env_actions
+    from gym_pbn_amd.network import load_network
+    from gym_pbn_amd.shard import gather_chunks, gather_rows, rows_digest, sampled_env_ids, shard_for
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = shard_for(rank, world, n_global // world)
+    net = load_network("bittner28")
+    o = O.Oracle(net)
+    st = o.step_philox(o.init_philox(sh.n_local, seed=7, env_base=sh.env_base), 7, sh.env_base, 0, T)
+    rows, bad = [], 0
+    for g in sampled_env_ids(sh.n_global, 16):
+        if sh.env_base <= g < sh.env_base + sh.n_local - 1:
+            mine = o.step_philox(o.init_philox(2, seed=7, env_base=g), 7, g, 0, T)
+            ref = np.ascontiguousarray(st[g - sh.env_base:g - sh.env_base + 2])
+            bad += 0 if np.array_equal(mine, ref) else 1
+            rows.append((g, ref.tobytes()))
+    all_rows = gather_rows(rows, dist)
+    acts = env_actions(5, sh.env_base, sh.n_local, 4, net.n_nodes).numpy()  # [T][B_local][A]
+    acts_all = gather_chunks(np.ascontiguousarray(acts.transpose(1, 0, 2)), dist)  # [B_global][T][A]
+    bad_t = torch.tensor([float(bad)])
+    dist.all_reduce(bad_t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        (Path(out_dir) / "digest.txt").write_text(f"{rows_digest(all_rows)} {len(all_rows)} {int(bad_t.item())}")
+        np.save(Path(out_dir) / "actions.npy", acts_all)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_check_digest_and_actions_same_at_world_1_and_2(tmp_path, oracle_mod):
+    n_global, T = 1000, 9
+    res = {}
+    for world in (1, 2):
+        d = tmp_path / f"w{world}"
+        d.mkdir()
+        mp.spawn(_digest_worker, args=(world, _free_port(), n_global, T, str(d)), nprocs=world, join=True)
+        dig, n, bad = (d / "digest.txt").read_text().split()
+        assert int(bad) == 0 and int(n) == 16  # every sampled pair re-run alone equals its shard's rows
+        res[world] = (dig, np.load(d / "actions.npy"))
+    assert res[1][0] == res[2][0]  # one digest for one global batch, at any rank count
+    assert np.array_equal(res[1][1], res[2][1])  # identical actions for the same global env ids
+    a = res[1][1]
+    assert a.shape == (n_global, 5, 4) and a.min() == 0 and a.max() <= 28 and 0.7 < (a == 0).mean() < 0.8
