@@ -352,10 +352,18 @@ def valu_roofline(v, s, updates):
     against the chip's VALU issue peak (64 lanes per wave-instruction)."""
     ipu = v["valu_wave_insts_per_update"]
     lane_ops = ipu * updates * 64
-    return {"bound": "valu", "achieved": lane_ops / s / 1e12, "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
-            "frac": lane_ops / s / 1e12 / VALU_PEAK_TOPS, "valu_wave_insts_per_update": ipu,
-            "valu_busy_frac": v.get("valu_busy_frac"), "kernel_s": s, "node_updates": updates,
-            "source": v.get("source", "profiles/r03_valu_pmc.json")}
+    out = {"bound": "valu", "achieved": lane_ops / s / 1e12, "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
+           "frac": lane_ops / s / 1e12 / VALU_PEAK_TOPS, "valu_wave_insts_per_update": ipu,
+           "frac_source": "issue slots: SQ_INSTS_VALU x 64 lane-ops per wave-instruction, masked lanes included",
+           "valu_busy_frac": v.get("valu_busy_frac"), "kernel_s": s, "node_updates": updates,
+           "source": v.get("source", "profiles/r04_valu_pmc.json")}
+    alf = v.get("active_lane_frac")
+    if alf is not None:  # useful work: lane-ops of enabled lanes only
+        out["active_lane_frac"] = alf
+        out["frac_active_lanes"] = out["frac"] * alf
+        out["frac_active_lanes_source"] = ("frac x active_lane_frac, active_lane_frac = SQ_THREAD_CYCLES_VALU / "
+                                           "(SQ_ACTIVE_INST_VALU x 64) from the same PMC pass (rocprofv3's VALUUtilization)")
+    return out
 
 
 def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather=True, check=False):

@@ -29,7 +29,7 @@ namespace pbn {
 // of the step kernel's phases, kept in registers and written once at the end of the wave.
 __device__ uint64_t g_stamps[16384 * 8];
 // k_env (cooperative-draw path): per wave, ENV_STAMPS words (tools/env_stamps.py reads them)
-constexpr int ENV_STAMPS = 32;
+constexpr int ENV_STAMPS = 40;
 __device__ uint64_t g_env_stamps[16384 * ENV_STAMPS];
 #endif
 
@@ -258,6 +258,33 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
         for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
         store_state<W>(a.state + eh * W, out);
     };
+#ifdef PBN_STEP_REGSEL
+    // Measurement variant: the four operand bits picked from the env's words in
+    // registers (word select by the node's word index, 64-bit shift), no plane writes; the selects'
+    // conditions depend on the record only, so they can be formed before the state lands
+    (void)eval;
+    auto bit_of = [&](const uint64_t (&s)[W], uint32_t n) -> uint32_t {
+        const uint32_t k = n >> 6;
+        uint64_t w = s[0];
+#pragma unroll
+        for (int q = 1; q < W; ++q) w = (k == (uint32_t)q) ? s[q] : w;
+        return (uint32_t)(w >> (n & 63u)) & 1u;
+    };
+    auto eval_r = [&](const uint64_t (&s)[W], uint32_t i, uint64_t r, uint32_t& own) {
+        own = bit_of(s, i);
+        const uint32_t p = (bit_of(s, (uint32_t)r & 0xFFFFu) << 3) | (bit_of(s, (uint32_t)(r >> 16) & 0xFFFFu) << 2) |
+                           (bit_of(s, (uint32_t)(r >> 32) & 0xFFFFu) << 1) | own;
+        return (uint32_t)(r >> (48 + p)) & 1u;
+    };
+    uint32_t own0, own1;
+    const uint32_t y0 = eval_r(cur, i0, r0, own0);
+#pragma unroll
+    for (int k = 0; k < W; ++k) asm volatile("" ::"v"(nxt[k]));
+    if (e < a.B && own0 != y0) put(cur, e, i0);
+    const uint32_t y1 = eval_r(nxt, i1, r1, own1);
+    if (e1 < a.B && own1 != y1) put(nxt, e1, i1);
+    (void)P;
+#else
     uint32_t self0, self1;
     const uint32_t y0 = eval(cur, i0, r0, self0);
     // env 0 is stored before env 1 is evaluated; env 1's loads (issued right behind env 0's) are waited
@@ -267,6 +294,7 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
     if (e < a.B && ((self0 >> (i0 & 31u)) & 1u) != y0) put(cur, e, i0);
     const uint32_t y1 = eval(nxt, i1, r1, self1);  // past B: junk from a clamped load, never stored
     if (e1 < a.B && ((self1 >> (i1 & 31u)) & 1u) != y1) put(nxt, e1, i1);
+#endif
 }
 
 // Step mode (T == 1, Philox; REPLAY == 0) and replay mode (REPLAY == 1: T updates from the
@@ -579,7 +607,8 @@ __device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* c
 
 __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
-constexpr uint32_t ENV_OWN_DRAWS_MIN = 40;  // active lanes from which a wave skips the shared draw tables
+constexpr uint32_t ENV_OWN_DRAWS_MIN = 40;
+constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many updates are resolved longest-first  // active lanes from which a wave skips the shared draw tables
 
 // ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
 struct RankMagic {
@@ -618,6 +647,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     constexpr bool TAIL = FAST == 4;      // wave-wide tail mode (see below)
     static_assert(!GEN || (KIND == KIND_PREDICTOR_MIX && !REPLAY), "GEN: predictor mix, Philox");
     extern __shared__ __align__(16) uint8_t lds[];
+#ifdef PBN_STAMPS
+    const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t N = (uint32_t)a.L.n_nodes;
     const Thr32 X = thr32_layout(a.L);
     if constexpr (GEN) {
@@ -673,6 +705,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     uint64_t est[ENV_STAMPS] = {};
     uint32_t ncapped = 0;
     est[0] = __builtin_amdgcn_s_memrealtime();
+    est[33] = rt_entry;  // kernel entry (before the image is staged); est[0] is after the staging barrier
 #endif
     const uint64_t* cubes = reinterpret_cast<const uint64_t*>(lds + a.off_cubes);
     const uint64_t* target = reinterpret_cast<const uint64_t*>(lds + a.off_target);
@@ -957,94 +990,218 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     tmode = true;
                 }
                 // envs beyond the one resolved next go to idle waves, if there are any
-                if (a.steal_local && (act & (act - 1ull)) != 0ull) local_push(act & (act - 1ull));
-                const uint32_t L = (uint32_t)__ffsll((unsigned long long)act) - 1u;
-                uint32_t u = (uint32_t)__shfl((int)used, (int)L);
-                uint32_t m = (uint32_t)__shfl((int)m_lo, (int)L);
-                const uint32_t h0 = (uint32_t)__shfl(hit0 ? 1 : 0, (int)L);
-                const uint64_t gid = a.env_base + (uint64_t)__shfl((long long)e, (int)L);
-                const uint32_t c1 = a.call_idx + (uint32_t)__shfl((int)t, (int)L);
+                // Which env first: the loop lengths are heavy-tailed (mean ~1,700 updates, longest ~62k at
+                // config 5's 2^20 cap), so an env that has already run long is the likeliest to run longest;
+                // it goes first (the others are the ones handed to idle waves), so the wave's last env is
+                // not the long one queued behind the rest. Lowest lane when none has run past ENV_LONG_USED.
+                uint32_t L = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+                if (__ballot(e >= 0 && used >= ENV_LONG_USED) != 0ull) {
+                    uint32_t mx = e >= 0 ? used : 0u;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+                    L = (uint32_t)__ffsll((unsigned long long)__ballot(e >= 0 && used == mx)) - 1u;
+                }
+                if (a.steal_local && (act & ~(1ull << L)) != 0ull) local_push(act & ~(1ull << L));
+                // the env's registers from lane L (wave-uniform index: v_readlane, no LDS permute)
+                auto from_L = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)L); };
+                uint32_t u = from_L(used);
+                uint32_t m = from_L(m_lo);
+                const uint32_t h0 = from_L(hit0 ? 1u : 0u);
+                const uint64_t gid = a.env_base + ((uint64_t)from_L((uint32_t)((uint64_t)e >> 32)) << 32 |
+                                                   (uint64_t)from_L((uint32_t)(uint64_t)e));
+                const uint32_t c1 = a.call_idx + from_L(t);
                 uint32_t* col = P.base + ((int32_t)L - (int32_t)lane);  // lane L's plane column
                 const uint8_t* colb = reinterpret_cast<const uint8_t*>(col);
                 const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
-                const uint32_t* ndl = reinterpret_cast<const uint32_t*>(ndelta);
+                uint8_t* const wmc = reinterpret_cast<uint8_t*>(wm);
                 const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;
-                auto last_writer = [&](uint64_t wmask) -> int32_t {
-                    const uint64_t w = wmask & below;
-                    return w ? 63 - (int32_t)__clzll((long long)w) : -1;
+                // predictor choice on the draw word (compact u32 thresholds, rows of tp4 <= 16: mode 2/4
+                // needs <= 16 predictors per node), as guarded straight-line reads rather than a loop
+                const uint32_t nq = X.tp4 >> 2;
+                auto tail_session = [&](auto one_row) {
+                // one_row: every node's thresholds fit one 16-B row (<= 5 predictors: Bittner-200), so a
+                // choice is one ds_read_b128 and the two choices of a Philox pair issue back to back
+                constexpr bool ONE_ROW = decltype(one_row)::value;
+                auto cnt4 = [](const uint4& t4, uint32_t a32) {
+                    return (a32 >= t4.x ? 1u : 0u) + (a32 >= t4.y ? 1u : 0u) + (a32 >= t4.z ? 1u : 0u) +
+                           (a32 >= t4.w ? 1u : 0u);
                 };
-                // A block's draws, records, counter deltas and in-block writers do not depend on the
-                // state: prepared one block ahead (speculatively at u + 64: a block that does not end
-                // the env step always applies all 64 updates), under the current block's resolution.
+                auto choice = [&](uint32_t i, uint32_t a32) -> uint32_t {
+                    const uint4* thr = reinterpret_cast<const uint4*>(lds) + (ONE_ROW ? i : i * nq);
+                    uint32_t j = cnt4(thr[0], a32);
+                    if (!ONE_ROW && nq > 1u) {
+                        j += cnt4(thr[1], a32);
+                        if (nq > 2u) {
+                            j += cnt4(thr[2], a32);
+                            if (nq > 3u) j += cnt4(thr[3], a32);
+                        }
+                    }
+                    return j;
+                };
+                // Philox with the key schedule recomputed per call (SALU adds): hoisted out of the block
+                // loop, its 20 round keys took SGPRs the kernel then spilled to VGPR lanes (v_readlane + nops)
+                auto draw = [&](uint32_t c0, uint32_t w4[4]) {
+                    uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                    asm volatile("" : "+s"(k0), "+s"(k1));
+                    w4[0] = c0;
+                    w4[1] = c1;
+                    w4[2] = (uint32_t)gid;
+                    w4[3] = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (STREAM_ENV << 24);
+                    philox4x32_10(w4, k0, k1);
+                };
+                // Draws. STREAM_ENV: update U of the env step takes Philox call U >> 1, words 2(U & 1) and
+                // 2(U & 1) + 1, so two blocks [ub, ub + 128) need 64 calls: lane k makes call (ub >> 1) + k
+                // once per pair of blocks and keeps both of its updates' env-record indices (u16 each);
+                // the pair's first block takes lane (k >> 1)'s, the second lane 32 + (k >> 1)'s, one
+                // ds_bpermute per block -- half the Philox work of one call per lane per block. A session
+                // starts at an even update (a lane-mode chunk boundary, ENV_CHUNK updates, or 0) and
+                // advances 64 per block; an odd start draws per lane (not expected).
+                //
+                // Software pipeline. A lone wave's block was bound by the latency of its dependent LDS
+                // round trips (draw index -> env record -> writer masks; stamps: ~1,400 cycles per block for
+                // ~210 instructions), so every state-independent stage works on a later block than the one
+                // being resolved and consumes a result issued one iteration earlier: resolving block k, the
+                // wave issues block k + 1's counter-delta read and writer-mask round, block k + 2's env-record
+                // read and block k + 3's draw (Philox every other block + ds_bpermute). Blocks after the one
+                // that ends the env step are speculative and dropped (the writer table is cleared in the same
+                // round that sets it, so it is all zero whenever a session ends).
+                const uint32_t u0 = u;
+                uint32_t epair = 0u;
+                const uint32_t pick_addr = (lane >> 1) * 4u, pick_sh = (lane & 1u) * 16u;
+                auto draw_idx = [&](uint32_t b) -> uint32_t {  // block b's env-record index, << pick_sh
+                    const uint32_t ub = u0 + 64u * b;
+                    if (u0 & 1u) {
+                        const uint32_t U = ub + lane;
+                        uint32_t w4[4];
+                        draw(U >> 1, w4);
+                        const uint32_t odd = U & 1u;
+                        const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
+                        return (__umul24(i, X.rs) + choice(i, odd ? w4[3] : w4[1])) << pick_sh;
+                    }
+                    if (!(b & 1u)) {
+                        uint32_t w4[4];
+                        draw((ub >> 1) + lane, w4);
+                        const uint32_t i0 = philox_node<KIND>(w4[0], N), i1 = philox_node<KIND>(w4[2], N);
+                        uint32_t j0, j1;
+                        if constexpr (ONE_ROW) {  // both rows read before either is compared
+                            const uint4 t0 = reinterpret_cast<const uint4*>(lds)[i0];
+                            const uint4 t1 = reinterpret_cast<const uint4*>(lds)[i1];
+                            j0 = cnt4(t0, w4[1]);
+                            j1 = cnt4(t1, w4[3]);
+                        } else {
+                            j0 = choice(i0, w4[1]);
+                            j1 = choice(i1, w4[3]);
+                        }
+                        epair = (__umul24(i0, X.rs) + j0) | ((__umul24(i1, X.rs) + j1) << 16);
+                    }
+                    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pick_addr + (b & 1u) * 128u), (int)epair);
+                };
+                auto erec_of = [&](uint32_t E) { return erec[(E >> pick_sh) & 0xFFFFu]; };
+                // Writer round of a block (its records q): node n's 64-bit writer mask at wmc + 8n, n = plane
+                // offset / 32 | bit (offset = dword * 1024); or, read the four operands' masks, clear.
+                struct WRound {
+                    uint32_t nd;
+                    uint64_t w0, w1, w2, wi;
+                };
+                auto wround = [&](const uint4& q) {
+                    WRound R;
+                    R.nd = *reinterpret_cast<const uint32_t*>(lds + (q.w >> 16));
+                    auto wadr = [&](uint32_t off, uint32_t bit) {
+                        return reinterpret_cast<unsigned long long*>(wmc + (off >> 2) + (bit << 3));
+                    };
+                    const uint32_t z = q.z;
+                    unsigned long long* const wi_p = wadr(q.y >> 16, z >> 24);
+                    atomicOr(wi_p, 1ull << lane);
+                    wave_sync();
+                    R.w0 = *wadr(q.x & 0xFFFFu, z & 31u);
+                    R.w1 = *wadr(q.x >> 16, (z >> 8) & 31u);
+                    R.w2 = *wadr(q.y & 0xFFFFu, (z >> 16) & 31u);
+                    R.wi = *wi_p;
+                    wave_sync();
+                    *wi_p = 0ull;  // the table is all zero again after every round
+                    return R;
+                };
+                //   hm: pattern bits (in0 8, in1 4, in2 2, own 1) whose operand an earlier lane of the
+                //       block writes; rr: that lane (the last such) per operand, in0 | in1 << 8 | in2 << 16 |
+                //       own << 24, i.e. the shift bringing its output to bit 0 of the block's ballot;
+                //   nx: the next lane writing this lane's node (~0: none) -- the commit's last-writer test.
                 struct TailDraw {
                     uint4 q;
-                    uint32_t nd;
-                    uint64_t wi;
-                    int32_t r0, r1, r2, r3;
+                    uint32_t nd, hm, rr, nx;
                 };
-                auto prepare = [&](uint32_t ub) {
+                auto writers = [&](const uint4& q, const WRound& R) {
                     TailDraw D;
-                    const uint32_t U = ub + lane;
-                    uint32_t w4[4];
-                    philox_draw(a.seed, U >> 1, c1, gid, STREAM_ENV, w4);
-                    const uint32_t odd = U & 1u;
-                    const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
-                    D.q = erec[__umul24(i, X.rs) + predictor_choice32(i, odd ? w4[3] : w4[1], lds, X.tp4)];
-                    constexpr uint32_t ROW = BLOCK * 4u;  // env_record's plane offsets: dword * ROW
-                    const uint32_t n0 = ((D.q.x & 0xFFFFu) / ROW) * 32u | (D.q.z & 31u),
-                                   n1 = ((D.q.x >> 16) / ROW) * 32u | ((D.q.z >> 8) & 31u),
-                                   n2 = ((D.q.y & 0xFFFFu) / ROW) * 32u | ((D.q.z >> 16) & 31u);
-                    D.nd = ndl[2u * i];
-                    atomicOr(reinterpret_cast<unsigned long long*>(&wm[i]), 1ull << lane);
-                    wave_sync();
-                    const uint64_t w0 = wm[n0], w1 = wm[n1], w2 = wm[n2];
-                    D.wi = wm[i];
-                    wave_sync();
-                    wm[i] = 0ull;  // the table is all zero again after every block
-                    D.r0 = last_writer(w0);
-                    D.r1 = last_writer(w1);
-                    D.r2 = last_writer(w2);
-                    D.r3 = last_writer(D.wi);
+                    D.q = q;
+                    D.nd = R.nd;
+                    uint32_t hm = 0u, rr = 0u;
+                    auto lw = [&](uint64_t w, uint32_t pbit, uint32_t sh) {
+                        const uint64_t wb = w & below;
+                        hm |= (wb != 0ull ? pbit : 0u);
+                        rr |= ((63u - (uint32_t)__clzll((long long)wb)) & 63u) << sh;
+                    };
+                    lw(R.w0, 8u, 0u);
+                    lw(R.w1, 4u, 8u);
+                    lw(R.w2, 2u, 16u);
+                    lw(R.wi, 1u, 24u);
+                    D.hm = hm;
+                    D.rr = rr;
+                    D.nx = (uint32_t)__ffsll((unsigned long long)(R.wi & ~upto)) - 1u;
                     return D;
                 };
                 bool fin = false, hitf = false;
                 uint32_t nblk = 0;
-                TailDraw D = prepare(u);
-                while (!fin) {
+                // prologue: blocks 0 (ready), 1 (record read), 2 (draw index)
+                const uint32_t E0 = draw_idx(0u);
+                const uint32_t E1 = draw_idx(1u);
+                uint32_t E2 = draw_idx(2u);
+                const uint4 q0 = erec_of(E0);
+                uint4 q1 = erec_of(E1);
+                TailDraw D = writers(q0, wround(q0));
+                for (uint32_t k = 0; !fin; ++k) {
 #ifdef PBN_STAMPS
                     // tail block phases (shader clocks, s_memtime): 19 blocks, 20 cycles per block, 21 fixed-point
                     // rounds, 22 cycles of the resolution (fixed point), 23 cycles from the block's top to the
-                    // next block's draws prepared, 24..31 blocks by rounds (0..6, 7+)
+                    // later blocks' stages issued, 24..31 blocks by rounds (0..6, 7+)
                     const uint64_t c_top = __builtin_amdgcn_s_memtime();
+                    const uint64_t r_top = __builtin_amdgcn_s_memrealtime();  // 100 MHz: calibrates s_memtime
+                    if (!est[34]) est[34] = r_top;
                     uint32_t nround = 0;
 #endif
                     const uint4 q = D.q;
                     const uint32_t U = u + lane;
-                    const uint32_t o0 = q.x & 0xFFFFu, o1 = q.x >> 16, o2 = q.y & 0xFFFFu, os = q.y >> 16;
-                    const uint32_t ss = (q.z >> 24) & 31u;
+                    const uint32_t ss = q.z >> 24;
                     // block-start values of the operands (in0, in1, in2, own bit)
-                    const uint32_t b0 = *reinterpret_cast<const uint32_t*>(colb + o0);
-                    const uint32_t b1 = *reinterpret_cast<const uint32_t*>(colb + o1);
-                    const uint32_t b2 = *reinterpret_cast<const uint32_t*>(colb + o2);
-                    const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + os);
-                    const TailDraw Dn = prepare(u + 64u);  // while those reads are in flight
+                    const uint32_t b0 = *reinterpret_cast<const uint32_t*>(colb + (q.x & 0xFFFFu));
+                    const uint32_t b1 = *reinterpret_cast<const uint32_t*>(colb + (q.x >> 16));
+                    const uint32_t b2 = *reinterpret_cast<const uint32_t*>(colb + (q.y & 0xFFFFu));
+                    const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + (q.y >> 16));
+                    // later blocks' stages, while those reads are in flight
+                    const WRound R1 = wround(q1);           // block k + 1: writer round (record landed)
+                    const uint4 q2 = erec_of(E2);           // block k + 2: env record (index landed)
+                    const uint32_t E3 = draw_idx(k + 3u);   // block k + 3: draw index
 #ifdef PBN_STAMPS
                     const uint64_t c_prep = __builtin_amdgcn_s_memtime();
 #endif
-                    const uint32_t v0 = __builtin_amdgcn_ubfe(b0, q.z, 1), v1 = __builtin_amdgcn_ubfe(b1, q.z >> 8, 1),
-                                   v2 = __builtin_amdgcn_ubfe(b2, q.z >> 16, 1), v3 = __builtin_amdgcn_ubfe(b3, ss, 1);
+                    const uint32_t v3 = __builtin_amdgcn_ubfe(b3, ss, 1);
+                    const uint32_t p0 = (__builtin_amdgcn_ubfe(b0, q.z, 1) << 3) | (__builtin_amdgcn_ubfe(b1, q.z >> 8, 1) << 2) |
+                                        (__builtin_amdgcn_ubfe(b2, q.z >> 16, 1) << 1) | v3;
+                    uint32_t y = __builtin_amdgcn_ubfe(q.w, p0, 1);
                     uint32_t x3 = v3;
-                    uint32_t y = __builtin_amdgcn_ubfe(q.w, (v0 << 3) | (v1 << 2) | (v2 << 1) | v3, 1);
-                    if (__ballot(D.r0 >= 0 || D.r1 >= 0 || D.r2 >= 0 || D.r3 >= 0) != 0) {
+                    if (__ballot(D.hm != 0u) != 0) {
+                        // fixed point: operands with an in-block writer take its output from the ballot of
+                        // the previous round (bit rr_j), the others keep their block-start value (pf)
+                        const uint32_t pf = p0 & ~D.hm;
+                        const uint32_t r0 = D.rr & 63u, r1 = (D.rr >> 8) & 63u, r2 = (D.rr >> 16) & 63u, r3 = D.rr >> 24;
+                        const uint32_t k0 = (D.hm >> 3) & 1u, k1 = (D.hm >> 2) & 1u, k2 = (D.hm >> 1) & 1u, k3 = D.hm & 1u;
                         for (;;) {
 #ifdef PBN_STAMPS
                             ++nround;
 #endif
                             const uint64_t Y = __ballot(y != 0u);
-                            auto pick = [&](int32_t r, uint32_t v) { return r >= 0 ? (uint32_t)(Y >> r) & 1u : v; };
-                            x3 = pick(D.r3, v3);
-                            const uint32_t yn = __builtin_amdgcn_ubfe(
-                                q.w, (pick(D.r0, v0) << 3) | (pick(D.r1, v1) << 2) | (pick(D.r2, v2) << 1) | x3, 1);
+                            const uint32_t p = pf | (((uint32_t)(Y >> r0) & k0) << 3) | (((uint32_t)(Y >> r1) & k1) << 2) |
+                                               (((uint32_t)(Y >> r2) & k2) << 1) | ((uint32_t)(Y >> r3) & k3);
+                            const uint32_t yn = __builtin_amdgcn_ubfe(q.w, p, 1);
+                            x3 = p & 1u;
                             if (__ballot(yn != y) == 0) break;
                             y = yn;
                         }
@@ -1054,29 +1211,29 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
                     // packed counter deltas (+ d for 0 -> 1, - d for 1 -> 0), prefix over the block
                     const uint32_t sg = y - 1u;
-                    const uint32_t mk = m + wave_inclusive_add((((y ^ x3) ? D.nd : 0u) ^ sg) - sg);
+                    const uint32_t mk = m + wave_inclusive_add(((D.nd & (0u - (y ^ x3))) ^ sg) - sg);
                     const bool valid = U < a.update_cap;
                     const bool hk = (U == 0u && !a.first_tested) ? h0 != 0u : has_zero_byte(mk) != 0u;
                     const uint64_t SM = __ballot(valid && hk), VM = __ballot(valid);
                     const uint32_t nd = SM ? (uint32_t)__ffsll((unsigned long long)SM) : (uint32_t)__popcll(VM);
-                    const uint64_t within = nd >= 64u ? ~0ull : ((1ull << nd) - 1ull);
-                    // commit: the last writer of each node among the first nd updates, if it changed the bit
-                    if (lane < nd && (D.wi & ~upto & within) == 0ull && y != v3) {
-                        uint32_t* dw = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + os);
-                        if (y)
-                            atomicOr(dw, 1u << ss);
-                        else
-                            atomicAnd(dw, ~(1u << ss));
-                    }
-                    m = (uint32_t)__shfl((int)mk, (int)(nd - 1u));
+                    // commit: the last writer of each node among the first nd updates flips its bit if its
+                    // output differs from the block-start value (distinct nodes: distinct bits)
+                    if (lane < nd && D.nx >= nd && y != v3)
+                        atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + (q.y >> 16)), 1u << ss);
+                    m = (uint32_t)__builtin_amdgcn_readlane((int)mk, (int)(nd - 1u));
                     u += nd;
                     hitf = SM != 0ull;
                     fin = hitf || u >= a.update_cap;
-                    D = Dn;
+                    D = writers(q1, R1);  // block k + 1 ready (its masks landed during the resolution)
+                    q1 = q2;
+                    E2 = E3;
                     wave_sync();
 #ifdef PBN_STAMPS
                     {
                         const uint64_t c_end = __builtin_amdgcn_s_memtime();
+                        const uint64_t r_end = __builtin_amdgcn_s_memrealtime();
+                        est[32] += r_end - r_top;  // realtime ticks (10 ns) in tail blocks
+                        est[35] = r_end;
                         est[19] += 1;
                         est[20] += c_end - c_top;
                         est[21] += nround;
@@ -1097,6 +1254,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     capped = !hitf;
                     done = true;
                 }
+                };  // tail_session
+                if (nq == 1u)
+                    tail_session(std::true_type{});
+                else
+                    tail_session(std::false_type{});
             }
         }
         uint16_t* gbuf = nullptr;

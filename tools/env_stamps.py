@@ -27,7 +27,7 @@ from gym_pbn_amd import _lib  # noqa: E402
 from gym_pbn_amd.batch import EnvConfig, Net, PBNBatch, attractors_from_cubes  # noqa: E402
 from gym_pbn_amd.network import load_network  # noqa: E402
 
-NS = 32
+NS = 40
 PHASES = {0: "start", 1: "below_40_active", 2: "queue_empty", 3: "le32_active", 4: "le16_active",
           5: "le8_active", 6: "le2_active", 7: "end"}
 

@@ -22,7 +22,7 @@ from gym_pbn_amd import _lib  # noqa: E402
 from gym_pbn_amd.batch import EnvConfig, Net, PBNBatch, attractors_from_cubes  # noqa: E402
 from gym_pbn_amd.network import load_network  # noqa: E402
 
-NS = 32
+NS = 40
 
 
 def main():
@@ -63,13 +63,32 @@ def main():
         st = st.reshape(-1, NS).astype(np.float64)
         if t >= 1:  # the first launch warms up
             acc += st[st[:, 19] > 0].sum(axis=0)
-            per_step.append({"kernel_ms": ms, "max_updates": int(nup.max().item())})
+            live = st[st[:, 0] > 0]
+            t0 = live[:, 33].min()
+            tl = live[live[:, 19] > 0]
+            per_step.append({"kernel_ms": ms, "max_updates": int(nup.max().item()),
+                             # realtime (10 ns ticks) from the first wave's entry, us
+                             "staged_us_max": float((live[:, 0] - t0).max() / 100),
+                             "first_tail_block_us_p50": float(np.median(tl[:, 34] - t0) / 100) if len(tl) else None,
+                             "last_wave_end_us": float((live[:, 7] - t0).max() / 100),
+                             "most_tail_blocks_in_a_wave": int(tl[:, 19].max()) if len(tl) else 0,
+                             "that_wave_tail_us": float(tl[np.argmax(tl[:, 19]), 32] / 100) if len(tl) else None,
+                             # timelines (us from the first entry): entry, staged, first tail block, last tail
+                             # block end, wave end -- of the wave with the most blocks and of the last wave to end
+                             "longest_wave": [round(float((tl[np.argmax(tl[:, 19]), k] - t0) / 100), 2)
+                                              for k in (33, 0, 34, 35, 7)] if len(tl) else None,
+                             "last_wave": [round(float((live[np.argmax(live[:, 7]), k] - t0) / 100), 2) if
+                                           live[np.argmax(live[:, 7]), k] else None for k in (33, 0, 34, 35, 7)],
+                             "last_wave_blocks": int(live[np.argmax(live[:, 7]), 19]),
+                             "last_wave_received_envs": int(live[np.argmax(live[:, 7]), 15])})
     blocks = acc[19]
     out = {"mode": mode, "B": B, "update_cap": CAP, "env_kernel": b.info().get("env_kernel"),
            "tail_blocks": int(blocks), "steps": per_step}
     if blocks:
         out.update({
             "cycles_per_block": acc[20] / blocks,
+            "us_per_block_realtime": acc[32] / blocks / 100,
+            "memtime_ticks_per_us": acc[20] / (acc[32] / 100),
             "cycles_top_to_next_prepared": acc[23] / blocks,
             "cycles_fixed_point": acc[22] / blocks,
             "cycles_rest": (acc[20] - acc[22] - acc[23]) / blocks,

@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
-"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r03_valu_pmc.json (copied to
+"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r04_valu_pmc.json (copied to
 profiles/ after review; bench.py reads it for the rollout and config-5 rooflines).
 
-One rocprofv3 --pmc pass (kernel trace only; 4 SQ counters + 1 GRBM counter, within one pass's
+One rocprofv3 --pmc pass (kernel trace only; 5 SQ counters + 1 GRBM counter, within one pass's
 limits) over tools/valu_pmc_child.py, which runs the bench line's rollout (1M envs, T = 64) and
 config-5 R6 chunks (131,072 envs, T = 100; fused and one launch per env step) with the bench's
 seeds and logs every launch's node updates. Per kernel configuration:
   valu_wave_insts_per_update = sum SQ_INSTS_VALU / sum node updates (wave64 instructions)
   valu_busy_frac             = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (both quad-cycles; the share of
                                wave time spent issuing VALU)
+  active_lane_frac           = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64): the mean share of a
+                               wave's 64 lanes enabled in its VALU instructions (rocprofv3's derived
+                               VALUUtilization / 100); lane-ops x this = useful lane-ops
   effective_clock_GHz        = GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time (MI355X_MICROARCH.md
                                'DVFS give-back'; reads high on dispatches under ~0.3 ms)
 The first launch of each configuration is dropped (warm-up). Runs rocprofv3 as a CHILD process.
@@ -21,7 +24,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-COUNTERS = ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+COUNTERS = ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+            "GRBM_GUI_ACTIVE"]
 
 
 def main():
@@ -57,14 +61,15 @@ def main():
         res[key] = {"kernel": items[0][0]["name"], "launches": len(items), "node_updates": ups,
                     "valu_wave_insts_per_update": tot["SQ_INSTS_VALU"] / ups,
                     "valu_busy_frac": tot["SQ_ACTIVE_INST_VALU"] / max(tot["SQ_WAVE_CYCLES"], 1),
+                    "active_lane_frac": tot["SQ_THREAD_CYCLES_VALU"] / max(tot["SQ_ACTIVE_INST_VALU"] * 64, 1),
                     "effective_clock_GHz": (tot["GRBM_GUI_ACTIVE"] / 8 / wall / 1e9) if wall else None,
                     "profiled_kernel_s": wall, "counters": tot,
                     "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
     doc = {"kernels": res, "valu_peak": "256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s "
                                         "(MI355X_MICROARCH.md: chip parameters, wave scheduling)"}
-    (ROOT / "gpurun_out" / "r03_valu_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
-    print(json.dumps({k: {kk: v[kk] for kk in ("valu_wave_insts_per_update", "valu_busy_frac", "effective_clock_GHz",
-                                               "launches")} for k, v in res.items()}))
+    (ROOT / "gpurun_out" / "r04_valu_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
+    print(json.dumps({k: {kk: v[kk] for kk in ("valu_wave_insts_per_update", "valu_busy_frac", "active_lane_frac",
+                                               "effective_clock_GHz", "launches")} for k, v in res.items()}))
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@ sys.path.insert(0, str(ROOT / "gym-pbn-stac_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from gym_pbn_amd.actions import env_actions  # noqa: E402
 from gym_pbn_amd.batch import EnvConfig, Net, PBNBatch, attractors_from_cubes  # noqa: E402
 from gym_pbn_amd.network import load_network  # noqa: E402
 
@@ -32,10 +33,7 @@ def main():
     gnet = Net(net)
     cfg = EnvConfig(gnet, attractors_from_cubes(z["cube_care"], z["cube_value"], z["cube_attractor"], 199), horizon=T)
     dev = torch.device("cuda", 0)
-    g = torch.Generator(device=dev)
-    g.manual_seed(0xAC7)
-    v = torch.randint(1, 200, (T, B, A), device=dev, generator=g, dtype=torch.int32)
-    acts = (v * (torch.rand((T, B, A), device=dev, generator=g) >= 0.75)).to(torch.int32).contiguous()
+    acts = env_actions(T, 0, B, A, 199, seed=0xAC7, device=dev)  # bench.py r6_figure's actions (rank 0)
     outs = [torch.empty((T, B, gnet.n_words), dtype=torch.int64, device=dev),
             torch.empty((T, B), dtype=torch.int32, device=dev),
             torch.empty((T, B), dtype=torch.uint8, device=dev),
