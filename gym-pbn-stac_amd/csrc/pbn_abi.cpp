@@ -116,7 +116,9 @@ struct pbn_envcfg {
         void* image = nullptr;
         void* reset_care = nullptr;
         void* reset_value = nullptr;
+        void* gen_image = nullptr;  // k_env modes 2/4: the LDS image as staged (env_gen_image), built once
     };
+    std::vector<uint8_t> gen_image;  // host copy (erec_shift is fixed by the network and the cubes)
     std::map<int, Dev> dev;
     const Dev* on(int device) {
         std::lock_guard<std::mutex> g(mu);
@@ -1271,6 +1273,7 @@ void pbn_envcfg_destroy(pbn_envcfg* c) {
     for (auto& kv : c->dev) {
         (void)hipSetDevice(kv.first);
         if (kv.second.image) (void)hipFree(kv.second.image);
+        if (kv.second.gen_image) (void)hipFree(kv.second.gen_image);
         if (kv.second.reset_care) (void)hipFree(kv.second.reset_care);
         if (kv.second.reset_value) (void)hipFree(kv.second.reset_value);
     }
@@ -1333,6 +1336,52 @@ int pbn_get_n_steps(pbn_batch* b, int64_t* n_steps) {
 // Per-step call, Bittner-200, 1 MI355X (256 CUs): G = 8 beats lane mode up to 32k envs (0.21 vs
 // 0.33 ms at B = 1, 0.88 vs 1.99 ms at 8k, 1.85 vs 2.04 ms at 32k) and loses from 64k on (2.31 vs
 // 2.07 ms; 131k: 3.28 vs 2.60 ms) -- the crossover sits near 48k envs.
+// The LDS image of k_env's cooperative-draw modes (2 / 4), built on the host once per env config: the
+// thresholds re-expressed on the draw word (u32, rows of tp4, saturated), the cubes / target / counter
+// deltas moved up by erec_shift, and the 16-B env records (pbn_device.hpp env_record) in rows of rs,
+// slot tp4 holding the record a = 2^32 - 1 selects. The kernel used to build these itself from the u64
+// image in its prologue (dependent global reads in every workgroup: ~8 us of a 63 us lone-env launch);
+// now it stages them with plain 16-B copies. Same bytes as the kernel's construction (every R6 test).
+static std::vector<uint8_t> env_gen_image(const pbn_envcfg* cfg, uint32_t erec_shift) {
+    const NetLayout& L = cfg->L;
+    const uint32_t N = (uint32_t)L.n_nodes, tp = L.tp, tp4 = (tp + 3u) & ~3u, rs = std::max(tp4 + 1u, L.pmax);
+    std::vector<uint8_t> g((size_t)L.bytes + erec_shift, 0);
+    const uint8_t* im = cfg->image.data();
+    auto thr = [&](uint32_t i, uint32_t q) -> uint64_t {  // u32_threshold of u64 threshold q of node i (2^32: never)
+        uint64_t T;
+        memcpy(&T, im + L.off_thr + 8 * ((size_t)i * tp + q), 8);
+        const uint64_t a0 = T >> 21;
+        if (a0 >= (1ull << 32)) return 1ull << 32;
+        return ((a0 << 21) | (a0 >> 11)) >= T ? a0 : a0 + 1u;
+    };
+    for (uint32_t i = 0; i < N; i++)
+        for (uint32_t q = 0; q < tp4; q++) {
+            const uint64_t t = q < tp ? thr(i, q) : (1ull << 32);
+            const uint32_t v = t >> 32 ? 0xFFFFFFFFu : (uint32_t)t;
+            memcpy(g.data() + 4 * ((size_t)i * tp4 + q), &v, 4);
+        }
+    memcpy(g.data() + cfg->off_cubes + erec_shift, im + cfg->off_cubes, L.bytes - cfg->off_cubes);
+    const uint32_t nd_off = cfg->off_ndelta + erec_shift, ROW = BLOCK * 4u;
+    auto off = [&](uint32_t x) { return (x >> 5) * ROW; };
+    for (uint32_t i = 0; i < N; i++)
+        for (uint32_t q = 0; q < rs; q++) {
+            uint32_t src = q;
+            if (q == tp4) {  // the node's thresholds below 2^32 on a
+                src = 0;
+                for (uint32_t p = 0; p < tp; p++) src += (thr(i, p) >> 32) ? 0u : 1u;
+            }
+            uint64_t rec = 0;
+            if (src < L.pmax) memcpy(&rec, im + L.off_rec + 8 * ((size_t)i * L.pmax + src), 8);
+            const uint32_t x0 = (uint32_t)rec & 0xFFFFu, x1 = (uint32_t)(rec >> 16) & 0xFFFFu,
+                           x2 = (uint32_t)(rec >> 32) & 0xFFFFu;
+            const uint32_t w[4] = {off(x0) | (off(x1) << 16), off(x2) | (off(i) << 16),
+                                   (x0 & 31u) | ((x1 & 31u) << 8) | ((x2 & 31u) << 16) | ((i & 31u) << 24),
+                                   (uint32_t)(rec >> 48) | ((nd_off + 8u * i) << 16)};
+            memcpy(g.data() + L.off_rec + 16 * ((size_t)i * rs + q), w, 16);
+        }
+    return g;
+}
+
 // Group mode (G = 8 lanes per env) for small batches -- except where the tail kernel (k_env mode 4:
 // <= 4 cubes and its 16-B env records fit) applies: its tail mode with one env per wave
 // (env_lane_limit) is faster at every batch size measured (profiles/r03_r6_lanes_sweep.json)
@@ -1377,6 +1426,17 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
             mode = 4;  // the same kernel with one packed counter word (<= 4 cubes)
     }
     if (mode != 2 && mode != 4) erec_shift = 0;
+    const void* gen_img = nullptr;
+    if ((mode == 2 || mode == 4) && (cfg->L.bytes + erec_shift) % 16u == 0u) {
+        std::lock_guard<std::mutex> g(cfg->mu);
+        if (cfg->gen_image.empty()) cfg->gen_image = env_gen_image(cfg, erec_shift);
+        auto& d = cfg->dev[b->device];  // on() above created it
+        if (!d.gen_image) {
+            HIP_TRY(hipMalloc(&d.gen_image, cfg->gen_image.size()));
+            HIP_TRY(hipMemcpy(d.gen_image, cfg->gen_image.data(), cfg->gen_image.size(), hipMemcpyHostToDevice));
+        }
+        gen_img = d.gen_image;
+    }
     int bpc = 1;
     if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc, b->net->N))
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
@@ -1391,6 +1451,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.n_updates = d_nup;
     a.error = b->d_error;
     a.img = dv->image;
+    a.gen_img = gen_img;
     a.L = cfg->L;
     a.off_cubes = cfg->off_cubes + erec_shift;
     a.off_target = cfg->off_target + erec_shift;

@@ -621,6 +621,17 @@ __constant__ constexpr RankMagic kRankMagic{};
 
 // Inclusive prefix sum over the wave's 64 lanes (row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast15 / row_bcast31 carry the row totals; lanes without a source add 0).
+// Inclusive max over the wave (the same DPP pattern; lanes without a source take 0): lane 63 holds the max.
+__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
@@ -652,7 +663,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
     const uint32_t N = (uint32_t)a.L.n_nodes;
     const Thr32 X = thr32_layout(a.L);
-    if constexpr (GEN) {
+    if (GEN && a.gen_img) {
+        // the host-built LDS image (pbn_abi.cpp env_gen_image): the same bytes as the construction below
+        stage_image(reinterpret_cast<const uint4*>(a.gen_img), (a.L.bytes + a.erec_shift) / 16, reinterpret_cast<uint4*>(lds));
+    } else if constexpr (GEN) {
         // LDS: the thresholds as staged; in place of the 8-B predictor records, 16-B "env
         // records" (EnvRec) carrying each input's plane offset and bit position, so an update
         // does no index arithmetic; the cubes / target / deltas after them move up by erec_shift
@@ -996,9 +1010,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // not the long one queued behind the rest. Lowest lane when none has run past ENV_LONG_USED.
                 uint32_t L = (uint32_t)__ffsll((unsigned long long)act) - 1u;
                 if (__ballot(e >= 0 && used >= ENV_LONG_USED) != 0ull) {
-                    uint32_t mx = e >= 0 ? used : 0u;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+                    const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_max(e >= 0 ? used : 0u), 63);
                     L = (uint32_t)__ffsll((unsigned long long)__ballot(e >= 0 && used == mx)) - 1u;
                 }
                 if (a.steal_local && (act & ~(1ull << L)) != 0ull) local_push(act & ~(1ull << L));
@@ -1056,15 +1068,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // ds_bpermute per block -- half the Philox work of one call per lane per block. A session
                 // starts at an even update (a lane-mode chunk boundary, ENV_CHUNK updates, or 0) and
                 // advances 64 per block; an odd start draws per lane (not expected).
-                //
-                // Software pipeline. A lone wave's block was bound by the latency of its dependent LDS
-                // round trips (draw index -> env record -> writer masks; stamps: ~1,400 cycles per block for
-                // ~210 instructions), so every state-independent stage works on a later block than the one
-                // being resolved and consumes a result issued one iteration earlier: resolving block k, the
-                // wave issues block k + 1's counter-delta read and writer-mask round, block k + 2's env-record
-                // read and block k + 3's draw (Philox every other block + ds_bpermute). Blocks after the one
-                // that ends the env step are speculative and dropped (the writer table is cleared in the same
-                // round that sets it, so it is all zero whenever a session ends).
+                // The next block is prepared (draw, record, writer round) while the current one resolves;
+                // it is speculative (dropped when the current block ends the env step; the writer table is
+                // cleared in the same round that sets it, so it is all zero whenever a session ends).
+                // Measured and not kept: a three-stage pipeline (block k + 1's writer round, k + 2's record,
+                // k + 3's draw issued while k resolves): a lone chain 0.0156 vs 0.0155 us per update, and
+                // 2-5 more VGPRs spilled in the lane-mode path (the kernel is at its 128-VGPR bound).
                 const uint32_t u0 = u;
                 uint32_t epair = 0u;
                 const uint32_t pick_addr = (lane >> 1) * 4u, pick_sh = (lane & 1u) * 16u;
@@ -1150,13 +1159,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 };
                 bool fin = false, hitf = false;
                 uint32_t nblk = 0;
-                // prologue: blocks 0 (ready), 1 (record read), 2 (draw index)
-                const uint32_t E0 = draw_idx(0u);
-                const uint32_t E1 = draw_idx(1u);
-                uint32_t E2 = draw_idx(2u);
-                const uint4 q0 = erec_of(E0);
-                uint4 q1 = erec_of(E1);
-                TailDraw D = writers(q0, wround(q0));
+                auto prepare = [&](uint32_t b) {
+                    const uint4 qb = erec_of(draw_idx(b));
+                    return writers(qb, wround(qb));
+                };
+                TailDraw D = prepare(0u);
                 for (uint32_t k = 0; !fin; ++k) {
 #ifdef PBN_STAMPS
                     // tail block phases (shader clocks, s_memtime): 19 blocks, 20 cycles per block, 21 fixed-point
@@ -1175,10 +1182,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint32_t b1 = *reinterpret_cast<const uint32_t*>(colb + (q.x >> 16));
                     const uint32_t b2 = *reinterpret_cast<const uint32_t*>(colb + (q.y & 0xFFFFu));
                     const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + (q.y >> 16));
-                    // later blocks' stages, while those reads are in flight
-                    const WRound R1 = wround(q1);           // block k + 1: writer round (record landed)
-                    const uint4 q2 = erec_of(E2);           // block k + 2: env record (index landed)
-                    const uint32_t E3 = draw_idx(k + 3u);   // block k + 3: draw index
+                    const TailDraw Dn = prepare(k + 1u);  // while those reads are in flight
 #ifdef PBN_STAMPS
                     const uint64_t c_prep = __builtin_amdgcn_s_memtime();
 #endif
@@ -1224,9 +1228,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     u += nd;
                     hitf = SM != 0ull;
                     fin = hitf || u >= a.update_cap;
-                    D = writers(q1, R1);  // block k + 1 ready (its masks landed during the resolution)
-                    q1 = q2;
-                    E2 = E3;
+                    D = Dn;
                     wave_sync();
 #ifdef PBN_STAMPS
                     {

@@ -118,6 +118,8 @@ struct EnvArgs {
                               // <= tail_max: every wave in tail mode from its first env)
     int32_t steal_local;      // fast == 4: hand-off of tail envs between the waves of a workgroup (LDS)
     uint32_t* steal_count;    // envs handed off in this launch (diagnostics), zeroed per launch
+    const void* gen_img;      // fast == 2 / 4: the LDS image as staged (host-built, pbn_abi.cpp env_gen_image);
+                              // null: the kernel builds it from img
 };
 
 constexpr uint32_t MT_ROW = 624;
