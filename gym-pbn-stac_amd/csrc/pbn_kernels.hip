@@ -1164,6 +1164,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     return writers(qb, wround(qb));
                 };
                 TailDraw D = prepare(0u);
+#ifdef PBN_STAMPS
+                const uint64_t sess_rt = __builtin_amdgcn_s_memrealtime();
+                const uint32_t sess_u0 = u;
+#endif
                 for (uint32_t k = 0; !fin; ++k) {
 #ifdef PBN_STAMPS
                     // tail block phases (shader clocks, s_memtime): 19 blocks, 20 cycles per block, 21 fixed-point
@@ -1250,6 +1254,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         if (others) local_push(others);
                     }
                 }
+#ifdef PBN_STAMPS
+                if ((u - sess_u0) / 64u > est[37]) {  // the wave's longest session: start, blocks, end, prior updates
+                    est[36] = sess_rt;
+                    est[37] = (u - sess_u0) / 64u;
+                    est[38] = __builtin_amdgcn_s_memrealtime();
+                    est[39] = sess_u0;
+                }
+#endif
                 if (lane == L) {
                     used = u;
                     m_lo = m;

@@ -80,6 +80,13 @@ def main():
                              "last_wave": [round(float((live[np.argmax(live[:, 7]), k] - t0) / 100), 2) if
                                            live[np.argmax(live[:, 7]), k] else None for k in (33, 0, 34, 35, 7)],
                              "last_wave_blocks": int(live[np.argmax(live[:, 7]), 19]),
+                             # the longest tail session of the launch (one env step of one env): start / end us,
+                             # blocks, updates the env had made before it (lane mode or earlier sessions)
+                             "longest_session": (lambda w: {"start_us": round(float((w[36] - t0) / 100), 1),
+                                                            "end_us": round(float((w[38] - t0) / 100), 1),
+                                                            "blocks": int(w[37]), "updates_before": int(w[39]),
+                                                            "wave_end_us": round(float((w[7] - t0) / 100), 1)})(
+                                 live[np.argmax(live[:, 37])]),
                              "last_wave_received_envs": int(live[np.argmax(live[:, 7]), 15])})
     blocks = acc[19]
     out = {"mode": mode, "B": B, "update_cap": CAP, "env_kernel": b.info().get("env_kernel"),
