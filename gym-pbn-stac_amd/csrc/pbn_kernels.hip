@@ -607,7 +607,10 @@ __device__ __forceinline__ bool attracting_plane(const P_t& P, const uint64_t* c
 
 __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
-constexpr uint32_t ENV_OWN_DRAWS_MIN = 40;
+#ifndef PBN_ENV_OWN_DRAWS_MIN
+#define PBN_ENV_OWN_DRAWS_MIN 40  // measurement builds (tools/build_exp.sh) change this
+#endif
+constexpr uint32_t ENV_OWN_DRAWS_MIN = PBN_ENV_OWN_DRAWS_MIN;
 constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many updates are resolved longest-first  // active lanes from which a wave skips the shared draw tables
 
 // ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
@@ -1290,10 +1293,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // ---- cooperative draw generation for the next ENV_CHUNK updates of every active lane
             uint8_t* gw = lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES;
             gbuf = reinterpret_cast<uint16_t*>(gw);                                   // [ENV_CHUNK][64]
-            uint8_t* lane_of_rank = gw + ENV_CHUNK * 128;                             // [64]
-            uint32_t* used_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64);  // [64]
-            uint64_t* gid_tab = reinterpret_cast<uint64_t*>(gw + ENV_CHUNK * 128 + 64 + 256);  // [64]
-            uint32_t* call_tab = reinterpret_cast<uint32_t*>(gw + ENV_CHUNK * 128 + 64 + 256 + 512);  // [64]
+            uint4* ctr_tab = reinterpret_cast<uint4*>(gw + ENV_CHUNK * 128 + 64);  // [64] by rank
+            auto cnt4 = [](const uint4& t4, uint32_t a32) {
+                return (a32 >= t4.x ? 1u : 0u) + (a32 >= t4.y ? 1u : 0u) + (a32 >= t4.z ? 1u : 0u) + (a32 >= t4.w ? 1u : 0u);
+            };
             const uint32_t nact = (uint32_t)__popcll(act);
             if (nact >= ENV_OWN_DRAWS_MIN) {
                 // (nearly) every lane active: each lane draws its own entries from its registers
@@ -1302,6 +1305,44 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // round costs two dependent LDS round trips more)
                 // (a chunk starts at an even update index: one Philox call per pair of updates)
                 const uint64_t gid = a.env_base + (uint64_t)e;
+#ifndef PBN_GEN_GENERIC
+                if (X.tp4 == 4u) {
+                    // one threshold row per node (<= 5 predictors: Bittner-200): four updates (two Philox
+                    // calls) per iteration with their four 16-B rows read back to back, so one LDS wait
+                    // serves four choices (the generic loop below waited once per choice), and the round
+                    // keys recomputed per call by SALU adds (hoisted, the 20 keys took SGPRs the kernel
+                    // spilled to VGPR lanes: a v_readlane and s_nop per round)
+                    const uint4* thr = reinterpret_cast<const uint4*>(lds);
+                    const uint32_t c1 = a.call_idx + t;
+                    const uint32_t g2 = (uint32_t)gid, g3 = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (STREAM_ENV << 24);
+                    for (uint32_t sl = 0; sl < ENV_CHUNK; sl += 4) {
+                        uint32_t w[8];
+#pragma unroll
+                        for (uint32_t p = 0; p < 2; ++p) {
+                            uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                            asm volatile("" : "+s"(k0), "+s"(k1));
+                            w[4 * p] = ((used + sl) >> 1) + p;
+                            w[4 * p + 1] = c1;
+                            w[4 * p + 2] = g2;
+                            w[4 * p + 3] = g3;
+                            philox4x32_10(w + 4 * p, k0, k1);
+                        }
+                        uint32_t i[4];
+                        uint4 t4[4];
+#pragma unroll
+                        for (uint32_t h = 0; h < 4; ++h) i[h] = philox_node<KIND>(w[2 * h], N);
+#pragma unroll
+                        for (uint32_t h = 0; h < 4; ++h) t4[h] = thr[i[h]];
+#pragma unroll
+                        for (uint32_t h = 0; h < 4; ++h) {
+                            const uint32_t j = cnt4(t4[h], w[2 * h + 1]);
+                            uint32_t ir = __umul24(i[h], X.rs);
+                            asm volatile("" : "+v"(ir));  // else folded with + j into a quarter-rate v_mad_u64_u32
+                            gbuf[(sl + h) * 64 + lane] = (uint16_t)(ir + j);
+                        }
+                    }
+                } else
+#endif
                 for (uint32_t sl = 0; sl < ENV_CHUNK; sl += 2) {
                     uint32_t w[4];
                     philox_draw(a.seed, (used + sl) >> 1, a.call_idx + t, gid, STREAM_ENV, w);
@@ -1313,11 +1354,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                 }
             } else {
+            // shared rounds: the active lanes' Philox counters in a table by rank (the lane id in the
+            // stream byte, which is the constant STREAM_ENV), so a round's counter is one 16-B read
+            // (before: the rank's lane, then its used / call / gid entries: two dependent round trips)
             if (e >= 0) {
-                lane_of_rank[__popcll(act & ((1ull << lane) - 1ull))] = (uint8_t)lane;
-                used_tab[lane] = used;
-                gid_tab[lane] = a.env_base + (uint64_t)e;
-                call_tab[lane] = a.call_idx + t;
+                const uint64_t gid = a.env_base + (uint64_t)e;
+                ctr_tab[__popcll(act & ((1ull << lane) - 1ull))] =
+                    make_uint4(used >> 1, a.call_idx + t, (uint32_t)gid, ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (lane << 24));
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1326,21 +1369,39 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // k / nact as a multiply-high by ceil(2^32 / nact): exact for k < 2^16 (nact == 1 handled apart,
             // its multiplier 2^32 does not fit 32 bits)
             const uint32_t magic = kRankMagic.v[nact];  // a 64-bit divide here was ~120 scalar instructions
-            for (uint32_t k0 = 0; k0 < total; k0 += 64) {
-                const uint32_t k = k0 + lane;
-                if (k < total) {
-                    const uint32_t sp = nact > 1 ? __umulhi(k, magic) : k, r = k - sp * nact;
-                    const uint32_t q = lane_of_rank[r];
-                    uint32_t w[4];
-                    philox_draw(a.seed, (used_tab[q] >> 1) + sp, call_tab[q], gid_tab[q], STREAM_ENV, w);
-#pragma unroll
-                    for (uint32_t h = 0; h < 2; ++h) {
-                        const uint32_t i = philox_node<KIND>(w[2 * h], N);
-                        const uint32_t j = predictor_choice32(i, w[2 * h + 1], lds, X.tp4);
-                        gbuf[(2 * sp + h) * 64 + q] = (uint16_t)(__umul24(i, X.rs) + j);
+            auto rounds = [&](auto one_row) {
+                for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+                    const uint32_t k = k0 + lane;
+                    if (k < total) {
+                        const uint32_t sp = nact > 1 ? __umulhi(k, magic) : k, r = k - sp * nact;
+                        const uint4 cr = ctr_tab[r];
+                        const uint32_t q = cr.w >> 24;
+                        uint32_t w[4] = {cr.x + sp, cr.y, cr.z, (cr.w & 0xFFFFFFu) | (STREAM_ENV << 24)};
+                        uint32_t k0s = (uint32_t)a.seed, k1s = (uint32_t)(a.seed >> 32);
+                        asm volatile("" : "+s"(k0s), "+s"(k1s));  // round keys by SALU adds (no spilled keys)
+                        philox4x32_10(w, k0s, k1s);
+                        const uint32_t i0 = philox_node<KIND>(w[0], N), i1 = philox_node<KIND>(w[2], N);
+                        uint32_t j0, j1;
+                        if constexpr (decltype(one_row)::value) {
+                            const uint4* thr = reinterpret_cast<const uint4*>(lds);
+                            const uint4 t0 = thr[i0], t1 = thr[i1];  // both rows in flight: one LDS wait
+                            j0 = cnt4(t0, w[1]);
+                            j1 = cnt4(t1, w[3]);
+                        } else {
+                            j0 = predictor_choice32(i0, w[1], lds, X.tp4);
+                            j1 = predictor_choice32(i1, w[3], lds, X.tp4);
+                        }
+                        uint32_t r0 = __umul24(i0, X.rs), r1 = __umul24(i1, X.rs);
+                        asm volatile("" : "+v"(r0), "+v"(r1));  // else folded with + j into v_mad_u64_u32
+                        gbuf[(2 * sp) * 64 + q] = (uint16_t)(r0 + j0);
+                        gbuf[(2 * sp + 1) * 64 + q] = (uint16_t)(r1 + j1);
                     }
                 }
-            }
+            };
+            if (X.tp4 == 4u)
+                rounds(std::true_type{});
+            else
+                rounds(std::false_type{});
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1366,7 +1427,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             auto nd_at = [&](const uint4& q) { return *reinterpret_cast<const uint2*>(lds + (q.w >> 16)); };
             uint2 n0 = nd_at(q0);
             uint32_t e2 = gbuf[128 + lane];
-            static_assert(ENV_CHUNK >= 3 && ENV_CHUNK % ENV_UNROLL == 0, "prefetch depth / unroll");
+            static_assert(ENV_CHUNK >= 3 && ENV_CHUNK % ENV_UNROLL == 0 && ENV_CHUNK % 4 == 0, "prefetch depth / unroll / draws");
             // Update c's counter update and attractor test are made after update c + 1's plane
             // reads are issued, while they are in flight: they only decide whether c + 1 is
             // applied (its act), so the dependent chain from one plane write to the next is the

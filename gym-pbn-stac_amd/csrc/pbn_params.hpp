@@ -214,7 +214,9 @@ constexpr uint32_t ENV_TAIL_DEFAULT = 16;
 // slot; e.g. 8,192 envs, cap 4,096: 0.19 vs 0.96 ms per step); at 32,768 the spec attractors' per-step
 // line is 31 % slower (short env steps queue behind long ones in one wave), so 6 per slot
 constexpr uint64_t ENV_ONE_LANE_ENVS_PER_SLOT = 6;
-constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 4 + 64 * 8 + 64 * 4;
+// a wave's draw buffer: the draw table [ENV_CHUNK][64] u16, 64 B (the hand-off flag in tail mode), the
+// shared rounds' counter table [64] uint4 by rank (the hand-off box in tail mode)
+constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 16;
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 uint32_t ssd_block(const SSDArgs& a);
