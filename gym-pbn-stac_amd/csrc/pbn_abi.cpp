@@ -154,6 +154,7 @@ struct pbn_batch {
     int env_lanes = 0;  // lanes per env of the last R6 launch
     int env_grid_last = 0;  // workgroups of the last R6 launch
     int env_lane_limit_last = 0;  // lanes per wave taking envs in the last R6 launch
+    int env_chunk_last = 0;       // draw-round chunk of the last R6 launch
     int env_kernel_last = -1;  // pbn_batch_info.env_kernel of the last R6 launch
     uint64_t* d_state = nullptr;
     int64_t* d_nsteps = nullptr;
@@ -167,6 +168,7 @@ struct pbn_batch {
     bool env_no_gen = false;  // PBNSIM_ENV_NO_GEN: no cooperative draw generation
     int env_group = 0;        // PBNSIM_ENV_GROUP: lanes per env (1 = lane mode), 0 = by batch size
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
+    int env_chunk = 0;        // PBNSIM_ENV_CHUNK: draw-round chunk 32 / 48 of the cooperative-draw kernels, 0 = auto
     int env_grid_cap = 0;     // PBNSIM_ENV_GRID: cap on the R6 kernel's workgroups (tests: lane refill), 0 = none
     int env_tail = -1;        // PBNSIM_ENV_TAIL: the R6 kernel's tail-mode threshold (live envs per wave), -1 = default
     int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
@@ -523,6 +525,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     b->env_no_gen = getenv("PBNSIM_ENV_NO_GEN") != nullptr;
     if (const char* v = getenv("PBNSIM_ENV_GROUP")) b->env_group = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_BPC")) b->env_bpc = std::max(1, atoi(v));
+    if (const char* v = getenv("PBNSIM_ENV_CHUNK")) b->env_chunk = atoi(v);
     if (const char* v = getenv("PBNSIM_ENV_GRID")) b->env_grid_cap = std::max(1, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_TAIL")) b->env_tail = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_LANES")) b->env_lane_limit = std::max(0, std::min(64, atoi(v)));
@@ -621,6 +624,7 @@ int pbn_batch_get_info(const pbn_batch* b, pbn_batch_info* info) {
     info->env_kernel = b->env_kernel_last;
     info->env_lane_limit = b->env_lane_limit_last;
     info->env_handoff = b->steal_last ? 1 : 0;
+    info->env_chunk = b->env_chunk_last;
     return 0;
 }
 
@@ -1410,7 +1414,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         const uint32_t tp4 = (cfg->L.tp + 3u) & ~3u;
         const uint32_t nrec = (uint32_t)b->net->N * std::max(tp4 + 1u, cfg->L.pmax);
         erec_shift = cfg->L.off_rec + 16u * nrec - cfg->off_cubes;
-        erec_fits = nrec <= 65535u && env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1) <= 64u * 1024u;
+        erec_fits = nrec <= 65535u &&
+                    env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1, 0, ENV_CHUNK_SMALL) <= 64u * 1024u;
     }
     // group mode (k_env_grp: G lanes per env, G updates per round trip; its rows need no env records)
     int grp = 1;
@@ -1438,8 +1443,29 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         gen_img = d.gen_image;
     }
     int bpc = 1;
-    if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc, b->net->N))
+    uint32_t chunk = ENV_CHUNK_SMALL;
+    if (mode == 2 || mode == 4) {
+        // the draw-round chunk (pbn_params.hpp ENV_CHUNK_SMALL / _LARGE): the large one unless the small
+        // one's draw buffers let more workgroups onto a CU and the launch is a throughput-bound fused run
+        // (>= 16 env steps per env over a queue of >= 4 envs per lane of the large one's grid), or the large
+        // one does not fit one workgroup's 64 KiB; PBNSIM_ENV_CHUNK=32 / 48 overrides
+        int bpc_s = 1, bpc_l = 1;
+        const uint32_t img = cfg->L.bytes + erec_shift;
+        if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, img, &bpc_s, b->net->N, ENV_CHUNK_SMALL))
+            return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
+        const bool large_fits = env_lds_bytes(b->W, img, mode, 1, 0, ENV_CHUNK_LARGE) <= 64u * 1024u;
+        if (large_fits)
+            if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, img, &bpc_l, b->net->N, ENV_CHUNK_LARGE))
+                return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
+        const uint64_t lanes_l = (uint64_t)b->n_cu * (uint64_t)bpc_l * BLOCK;
+        const bool throughput = n_calls >= 16u && b->B >= 4u * lanes_l && bpc_s > bpc_l;
+        chunk = large_fits && !throughput ? ENV_CHUNK_LARGE : ENV_CHUNK_SMALL;
+        if (b->env_chunk == (int)ENV_CHUNK_SMALL || (b->env_chunk == (int)ENV_CHUNK_LARGE && large_fits))
+            chunk = (uint32_t)b->env_chunk;
+        bpc = chunk == ENV_CHUNK_LARGE ? bpc_l : bpc_s;
+    } else if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, cfg->L.bytes + erec_shift, &bpc, b->net->N)) {
         return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
+    }
     if (b->env_bpc) bpc = std::min(bpc, b->env_bpc);
     EnvArgs a{};
     a.state = b->d_state;
@@ -1471,6 +1497,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     }
     a.fast = mode;
     a.grp = grp;
+    a.chunk = chunk;
     a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + erec_shift + 8u * (uint32_t)b->W * BLOCK;
     if (int rc = b->s_counter.ensure(8)) return rc;
     a.counter = (unsigned long long*)b->s_counter.p;
@@ -1516,6 +1543,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     b->env_lanes = grp;
     b->env_grid_last = grid;
     b->env_lane_limit_last = (int)a.lane_limit;
+    b->env_chunk_last = (a.fast == 2 || a.fast == 4) ? (int)a.chunk : 0;
     b->env_kernel_last = replay ? std::min(mode, 1) : mode;
     return 0;
 }

@@ -647,12 +647,14 @@ __device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
 
 
 
-// A wave's draw buffer (ENV_GEN_WAVE_BYTES) in tail mode: the per-node 64-bit writer masks from byte
-// 0 (N <= 512 nodes: 4 KiB), the hand-off flag at ENV_CHUNK * 128 and the hand-off box (5 + 2W words)
-// 64 B after it; lane mode's draw table [ENV_CHUNK][64] u16 and rank / counter tables use the same bytes
-static_assert(8u * 512u <= ENV_CHUNK * 128u, "tail writer masks (N <= 512) overlap the hand-off flag");
-static_assert(ENV_CHUNK * 128u + 64u + 8u * (5u + 2u * 8u) <= ENV_GEN_WAVE_BYTES,
+// A wave's draw buffer (env_gen_wave_bytes(chunk)) in tail mode: the per-node 64-bit writer masks from
+// byte 0 (N <= 512 nodes: 4 KiB), the hand-off flag at chunk * 128 and the hand-off box (5 + 2W words)
+// 64 B after it; lane mode's draw table [chunk][64] u16 and counter table use the same bytes
+static_assert(8u * 512u <= ENV_CHUNK_SMALL * 128u, "tail writer masks (N <= 512) overlap the hand-off flag");
+static_assert(ENV_CHUNK_SMALL * 128u + 64u + 8u * (5u + 2u * 8u) <= env_gen_wave_bytes(ENV_CHUNK_SMALL),
               "the hand-off box (W <= 8) overflows the wave's draw buffer");
+static_assert(ENV_CHUNK_SMALL % 8u == 0 && ENV_CHUNK_LARGE % 8u == 0 && ENV_UNROLL == 8u,
+              "draw-round chunks: multiples of the unroll (and of 4: the own-draw iteration)");
 
 template <int W, int KIND, int REPLAY, int FAST>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_env(EnvArgs a) {
@@ -706,7 +708,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     }
     // workgroup hand-off (TAIL, steal_local): control words after the draw buffers (busy waves, idle
     // mask); each wave's mailbox flag sits in its own draw buffer's table region (cleared on going idle)
-    uint32_t* const wctl = reinterpret_cast<uint32_t*>(lds + a.off_gen + (BLOCK / 64) * ENV_GEN_WAVE_BYTES);
+    // the launch's draw-round chunk (GEN) and the per-wave draw buffer it sizes
+    const uint32_t CH = GEN ? a.chunk : ENV_CHUNK;
+    const uint32_t GWB = env_gen_wave_bytes(CH);
+    uint32_t* const wctl = reinterpret_cast<uint32_t*>(lds + a.off_gen + (BLOCK / 64) * GWB);
     if (TAIL && a.steal_local && threadIdx.x == 0) {
         wctl[0] = BLOCK / 64;  // busy
         wctl[1] = 0u;          // idle mask
@@ -762,10 +767,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     // pushers stalled for milliseconds behind them).
     const uint32_t wv_in_wg = threadIdx.x >> 6;
     auto box_of = [&](uint32_t w) {
-        return reinterpret_cast<uint64_t*>(lds + a.off_gen + w * ENV_GEN_WAVE_BYTES + ENV_CHUNK * 128 + 64);
+        return reinterpret_cast<uint64_t*>(lds + a.off_gen + w * GWB + CH * 128 + 64);
     };
     auto flag_of = [&](uint32_t w) {
-        return reinterpret_cast<uint32_t*>(lds + a.off_gen + w * ENV_GEN_WAVE_BYTES + ENV_CHUNK * 128);
+        return reinterpret_cast<uint32_t*>(lds + a.off_gen + w * GWB + CH * 128);
     };
     auto ldl = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
     auto local_push = [&](uint64_t cand) {
@@ -1000,7 +1005,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // per block round trip instead of one per update.
             if (tmode || (__popcll(act) <= a.tail_max && __ballot(exhausted) != 0)) {
                 in_tail = true;
-                uint64_t* wm = reinterpret_cast<uint64_t*>(lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES);
+                uint64_t* wm = reinterpret_cast<uint64_t*>(lds + a.off_gen + (threadIdx.x >> 6) * GWB);
                 if (!tmode) {
                     for (uint32_t k = lane; k < N; k += 64) wm[k] = 0ull;
                     wave_sync();
@@ -1074,7 +1079,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // once per pair of blocks and keeps both of its updates' env-record indices (u16 each);
                 // the pair's first block takes lane (k >> 1)'s, the second lane 32 + (k >> 1)'s, one
                 // ds_bpermute per block -- half the Philox work of one call per lane per block. A session
-                // starts at an even update (a lane-mode chunk boundary, ENV_CHUNK updates, or 0) and
+                // starts at an even update (a lane-mode chunk boundary, CH updates, or 0) and
                 // advances 64 per block; an odd start draws per lane (not expected).
                 // The next block is prepared (draw, record, writer round) while the current one resolves;
                 // it is speculative (dropped when the current block ends the env step; the writer table is
@@ -1290,10 +1295,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         uint16_t* gbuf = nullptr;
         if (!in_tail) {
         if constexpr (GEN) {
-            // ---- cooperative draw generation for the next ENV_CHUNK updates of every active lane
-            uint8_t* gw = lds + a.off_gen + (threadIdx.x >> 6) * ENV_GEN_WAVE_BYTES;
-            gbuf = reinterpret_cast<uint16_t*>(gw);                                   // [ENV_CHUNK][64]
-            uint4* ctr_tab = reinterpret_cast<uint4*>(gw + ENV_CHUNK * 128 + 64);  // [64] by rank
+            // ---- cooperative draw generation for the next CH updates of every active lane
+            uint8_t* gw = lds + a.off_gen + (threadIdx.x >> 6) * GWB;
+            gbuf = reinterpret_cast<uint16_t*>(gw);                                   // [CH][64]
+            uint4* ctr_tab = reinterpret_cast<uint4*>(gw + CH * 128 + 64);  // [64] by rank
             auto cnt4 = [](const uint4& t4, uint32_t a32) {
                 return (a32 >= t4.x ? 1u : 0u) + (a32 >= t4.y ? 1u : 0u) + (a32 >= t4.z ? 1u : 0u) + (a32 >= t4.w ? 1u : 0u);
             };
@@ -1315,7 +1320,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint4* thr = reinterpret_cast<const uint4*>(lds);
                     const uint32_t c1 = a.call_idx + t;
                     const uint32_t g2 = (uint32_t)gid, g3 = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (STREAM_ENV << 24);
-                    for (uint32_t sl = 0; sl < ENV_CHUNK; sl += 4) {
+                    for (uint32_t sl = 0; sl < CH; sl += 4) {
                         uint32_t w[8];
 #pragma unroll
                         for (uint32_t p = 0; p < 2; ++p) {
@@ -1343,7 +1348,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                 } else
 #endif
-                for (uint32_t sl = 0; sl < ENV_CHUNK; sl += 2) {
+                for (uint32_t sl = 0; sl < CH; sl += 2) {
                     uint32_t w[4];
                     philox_draw(a.seed, (used + sl) >> 1, a.call_idx + t, gid, STREAM_ENV, w);
 #pragma unroll
@@ -1365,7 +1370,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t total = nact * (ENV_CHUNK / 2);  // pairs of updates: one Philox call each
+            const uint32_t total = nact * (CH / 2);  // pairs of updates: one Philox call each
             // k / nact as a multiply-high by ceil(2^32 / nact): exact for k < 2^16 (nact == 1 handled apart,
             // its multiplier 2^32 does not fit 32 bits)
             const uint32_t magic = kRankMagic.v[nact];  // a 64-bit divide here was ~120 scalar instructions
@@ -1409,7 +1414,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         }
         if (e < 0) continue;
 
-        // ---- up to ENV_CHUNK updates of this lane's env
+        // ---- up to CH updates of this lane's env
         const uint64_t g = a.env_base + (uint64_t)e;
         if constexpr (GEN) {
             const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
@@ -1427,7 +1432,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             auto nd_at = [&](const uint4& q) { return *reinterpret_cast<const uint2*>(lds + (q.w >> 16)); };
             uint2 n0 = nd_at(q0);
             uint32_t e2 = gbuf[128 + lane];
-            static_assert(ENV_CHUNK >= 3 && ENV_CHUNK % ENV_UNROLL == 0 && ENV_CHUNK % 4 == 0, "prefetch depth / unroll / draws");
             // Update c's counter update and attractor test are made after update c + 1's plane
             // reads are issued, while they are in flight: they only decide whether c + 1 is
             // applied (its act), so the dependent chain from one plane write to the next is the
@@ -1468,9 +1472,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // its remaining updates masked (act = 0: nothing is written); the test sees act before
             // the block's last update is settled, so a wave may run one masked block more.
             // The cap test is compiled in only for chunks where some lane of the wave can reach
-            // the cap (lim < ENV_CHUNK); the other chunks run the loop without it.
+            // the cap (lim < CH); the other chunks run the loop without it.
             auto chunk = [&](auto cap_near) {
-            for (uint32_t c0 = 0; c0 < ENV_CHUNK; c0 += ENV_UNROLL) {
+            for (uint32_t c0 = 0; c0 < CH; c0 += ENV_UNROLL) {
 #pragma unroll
             for (uint32_t u = 0; u < ENV_UNROLL; ++u) {
                 const uint32_t c = c0 + u;
@@ -1480,7 +1484,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 n0 = nd_at(q1);
                 q0 = q1;
                 q1 = erec[e2];
-                e2 = gbuf[min(c + 3, ENV_CHUNK - 1) * 64 + lane];
+                e2 = gbuf[min(c + 3, CH - 1) * 64 + lane];
                 // Predstep (base.py:100-118): Y = tt[x_in0 x_in1 x_in2 x_self] from the plane
                 const uint32_t b0 = *reinterpret_cast<const uint32_t*>(pb + (q.x & 0xFFFFu));
                 const uint32_t b1 = *reinterpret_cast<const uint32_t*>(pb + (q.x >> 16));
@@ -1506,7 +1510,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             }
             };
 
-            if (__ballot(lim < ENV_CHUNK) != 0)
+            if (__ballot(lim < CH) != 0)
                 chunk(std::true_type{});
             else
                 chunk(std::false_type{});
@@ -2227,7 +2231,7 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
                                               : env_fn_w<KIND_PROB_TABLE>(W, replay, a.fast, a.grp);
     EnvArgs c = a;
     return launch(fn, grid, env_lds_bytes(W, a.L.bytes + a.erec_shift, replay ? std::min(a.fast, 1) : a.fast, a.grp,
-                                          a.L.n_nodes),
+                                          a.L.n_nodes, a.chunk),
                   stream, &c, sizeof c);
 }
 
@@ -2250,18 +2254,18 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
     return occupancy(fn, sb, step_lds_bytes(W, lds_bytes, sb, grp), blocks_per_cu);
 }
 
-uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes) {
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes, uint32_t chunk) {
     if (fast == 3) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
     const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
     (void)n_nodes;
     // fast == 4: 16 B of workgroup hand-off control after the per-wave draw buffers
-    return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * ENV_GEN_WAVE_BYTES + (fast == 4 ? 16u : 0u) : planes;
+    return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * env_gen_wave_bytes(chunk) + (fast == 4 ? 16u : 0u) : planes;
 }
 
-int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes) {
+int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes, uint32_t chunk) {
     void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast, grp)
                                           : env_fn_w<KIND_PROB_TABLE>(W, 0, fast, grp);
-    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast, grp, n_nodes), blocks_per_cu);
+    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast, grp, n_nodes, chunk), blocks_per_cu);
 }
 
 }  // namespace pbn

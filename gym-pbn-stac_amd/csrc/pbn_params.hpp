@@ -120,6 +120,7 @@ struct EnvArgs {
     uint32_t* steal_count;    // envs handed off in this launch (diagnostics), zeroed per launch
     const void* gen_img;      // fast == 2 / 4: the LDS image as staged (host-built, pbn_abi.cpp env_gen_image);
                               // null: the kernel builds it from img
+    uint32_t chunk;           // fast == 2 / 4: updates per lane between draw rounds (ENV_CHUNK_SMALL / _LARGE)
 };
 
 constexpr uint32_t MT_ROW = 624;
@@ -193,8 +194,6 @@ int launch_flip(int W, const FlipArgs& a, int grid, void* stream);
 int launch_unpack(const uint64_t* words, uint8_t* out, uint64_t B, uint32_t N, uint32_t W, int grid, void* stream);
 int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream);
 int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per_cu, int rollout = 0, int grp = 1);
-int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes = 0);
-uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes = 0);
 
 #ifndef PBN_ENV_CHUNK
 #define PBN_ENV_CHUNK 32
@@ -214,9 +213,19 @@ constexpr uint32_t ENV_TAIL_DEFAULT = 16;
 // slot; e.g. 8,192 envs, cap 4,096: 0.19 vs 0.96 ms per step); at 32,768 the spec attractors' per-step
 // line is 31 % slower (short env steps queue behind long ones in one wave), so 6 per slot
 constexpr uint64_t ENV_ONE_LANE_ENVS_PER_SLOT = 6;
-// a wave's draw buffer: the draw table [ENV_CHUNK][64] u16, 64 B (the hand-off flag in tail mode), the
+// Cooperative-draw kernels (EnvArgs::fast 2 / 4) take their chunk (updates per lane between draw
+// rounds) per launch, EnvArgs::chunk: 48 by default -- fewer chunk prologues on the long per-lane
+// chains of a per-step launch (131,072 envs, cap 4,096: 1.22 -> 1.17 ms per step) -- and 32 where the
+// smaller draw buffers let one more workgroup onto a CU and the launch is throughput-bound (a fused
+// multi-step launch over a queue of several envs per lane: 1M envs, T = 100, 3.46 vs 4.05 ms per env
+// step); profiles/r04_r6_chunk_sweep.json
+constexpr uint32_t ENV_CHUNK_SMALL = 32, ENV_CHUNK_LARGE = 48;
+// a wave's draw buffer: the draw table [chunk][64] u16, 64 B (the hand-off flag in tail mode), the
 // shared rounds' counter table [64] uint4 by rank (the hand-off box in tail mode)
-constexpr uint32_t ENV_GEN_WAVE_BYTES = ENV_CHUNK * 64 * 2 + 64 + 64 * 16;
+constexpr uint32_t env_gen_wave_bytes(uint32_t chunk) { return chunk * 64u * 2u + 64u + 64u * 16u; }
+int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes = 0,
+                   uint32_t chunk = ENV_CHUNK_LARGE);
+uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes = 0, uint32_t chunk = ENV_CHUNK_LARGE);
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
 uint32_t ssd_block(const SSDArgs& a);

@@ -63,7 +63,7 @@ class BatchInfo(C.Structure):
         ("n_envs", C.c_uint64), ("env_id_base", C.c_uint64), ("seed", C.c_uint64), ("update_count", C.c_uint64),
         ("env_call_count", C.c_uint32), ("reset_count", C.c_uint32), ("mt_ready", C.c_int32),
         ("env_lanes", C.c_int32), ("roll_lanes", C.c_int32), ("env_grid", C.c_int32), ("env_kernel", C.c_int32),
-        ("env_lane_limit", C.c_int32), ("env_handoff", C.c_int32),
+        ("env_lane_limit", C.c_int32), ("env_handoff", C.c_int32), ("env_chunk", C.c_int32),
     ]
 
 

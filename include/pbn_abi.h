@@ -91,6 +91,8 @@ typedef struct {
     int32_t env_handoff;    /* last R6 env-step launch, env_kernel 4: 1 if a wave in tail mode could hand envs it had
                                not started on to idle waves of its workgroup (PBNSIM_ENV_STEAL=0 turns it off);
                                count: pbn_env_handoffs */
+    int32_t env_chunk;      /* last R6 env-step launch, env_kernel 2/4: updates per lane between draw rounds (32 or 48;
+                               PBNSIM_ENV_CHUNK overrides) */
 } pbn_batch_info;
 
 /* Attractor / goal description for the multi-flip env step (R6).

@@ -61,7 +61,7 @@ def child(B, T, spec, cap):
         n = outs[3].to(torch.int64)
         res["fused" if fused else "per_step"] = {"ms_per_env_step": best * 1e3 / T, "env_steps_per_s": B * T / best,
                                                  "max_updates": int(n.max()), "mean_updates": float(n.float().mean()),
-                                                "env_grid": inf["env_grid"], "env_lane_limit": inf["env_lane_limit"],
+                                                "env_grid": inf["env_grid"], "env_lane_limit": inf["env_lane_limit"], "env_chunk": inf.get("env_chunk"),
                                                 "handoffs_last_launch": handoffs}
     print(json.dumps(res))
 
