@@ -49,6 +49,20 @@ __device__ __forceinline__ void philox_draw(uint64_t seed, uint32_t c0, uint32_t
     philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// The same with the round keys recomputed by SALU adds at the call (seed must be wave-uniform): in a
+// kernel short of SGPRs, 20 hoisted round keys are spilled to VGPR lanes and every round pays a
+// v_readlane and a wait state (k_env's draw loops)
+__device__ __forceinline__ void philox_draw_sk(uint64_t seed, uint32_t c0, uint32_t c1, uint64_t gid, uint32_t stream,
+                                               uint32_t w[4]) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    asm volatile("" : "+s"(k0), "+s"(k1));
+    w[0] = c0;
+    w[1] = c1;
+    w[2] = (uint32_t)gid;
+    w[3] = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (stream << 24);
+    philox4x32_10(w, k0, k1);
+}
+
 // Draws of the step and R6 streams use two 32-bit words per update: the node word and the
 // predictor-choice uniform a, taken as k53 = a << 21 | a >> 11 (32 random bits spread over the
 // 53-bit grid, monotone in a, so the integer thresholds decide the choice exactly; choice

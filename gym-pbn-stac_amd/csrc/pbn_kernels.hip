@@ -1064,15 +1064,40 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     return j;
                 };
                 // Philox with the key schedule recomputed per call (SALU adds): hoisted out of the block
-                // loop, its 20 round keys took SGPRs the kernel then spilled to VGPR lanes (v_readlane + nops)
+                // loop, its 20 round keys took SGPRs the kernel then spilled to VGPR lanes (v_readlane + nops).
+                // the block's calls differ in counter word 0 only (words 1-3: the session's call index and
+                // env id), so half of rounds 0 and 1 is the same for every lane: computed once per session
+                // (scalar), a block's call is 18 multiplies instead of 20
+                const uint32_t sk0 = (uint32_t)a.seed, sk1 = (uint32_t)(a.seed >> 32);
+                const uint64_t P1u = (uint64_t)0xCD9E8D57u * (uint32_t)gid;
+                const uint32_t A0 = (uint32_t)(P1u >> 32) ^ c1 ^ sk0;
+                const uint32_t U0 = (((uint32_t)(gid >> 32) & 0xFFFFFFu) | (STREAM_ENV << 24)) ^ sk1;
+                const uint32_t V1 = (uint32_t)P1u ^ (sk0 + 0x9E3779B9u);
+                const uint64_t P0u = (uint64_t)0xD2511F53u * A0;
+                const uint32_t H1 = (uint32_t)(P0u >> 32) ^ (sk1 + 0xBB67AE85u), L1 = (uint32_t)P0u;
                 auto draw = [&](uint32_t c0, uint32_t w4[4]) {
-                    uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;  // round 0 (its other half: A0, lo(P1u))
+                    const uint32_t y = (uint32_t)(p0 >> 32) ^ U0;
+                    const uint64_t p1 = (uint64_t)0xCD9E8D57u * y;  // round 1 (its other half: H1, L1)
+                    w4[0] = (uint32_t)(p1 >> 32) ^ V1;
+                    w4[1] = (uint32_t)p1;
+                    w4[2] = (uint32_t)p0 ^ H1;
+                    w4[3] = L1;
+                    uint32_t k0 = sk0 + 0x9E3779B9u, k1 = sk1 + 0xBB67AE85u;
                     asm volatile("" : "+s"(k0), "+s"(k1));
-                    w4[0] = c0;
-                    w4[1] = c1;
-                    w4[2] = (uint32_t)gid;
-                    w4[3] = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (STREAM_ENV << 24);
-                    philox4x32_10(w4, k0, k1);
+#pragma unroll
+                    for (int r = 2; r < PBN_PHILOX_ROUNDS; ++r) {  // rounds 2.. as philox4x32_10
+                        k0 += 0x9E3779B9u;
+                        k1 += 0xBB67AE85u;
+                        const uint64_t q0 = (uint64_t)0xD2511F53u * w4[0];
+                        const uint64_t q1 = (uint64_t)0xCD9E8D57u * w4[2];
+                        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(k0, (uint32_t)(q1 >> 32), w4[1], 0x96);
+                        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(k1, (uint32_t)(q0 >> 32), w4[3], 0x96);
+                        w4[1] = (uint32_t)q1;
+                        w4[3] = (uint32_t)q0;
+                        w4[0] = n0;
+                        w4[2] = n2;
+                    }
                 };
                 // Draws. STREAM_ENV: update U of the env step takes Philox call U >> 1, words 2(U & 1) and
                 // 2(U & 1) + 1, so two blocks [ub, ub + 128) need 64 calls: lane k makes call (ub >> 1) + k
@@ -1098,7 +1123,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         draw(U >> 1, w4);
                         const uint32_t odd = U & 1u;
                         const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
-                        return (__umul24(i, X.rs) + choice(i, odd ? w4[3] : w4[1])) << pick_sh;
+                        uint32_t ir = __umul24(i, X.rs);
+                        asm volatile("" : "+v"(ir));  // else folded with the choice into a quarter-rate v_mad_u64_u32
+                        return (ir + choice(i, odd ? w4[3] : w4[1])) << pick_sh;
                     }
                     if (!(b & 1u)) {
                         uint32_t w4[4];
@@ -1319,19 +1346,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     // spilled to VGPR lanes: a v_readlane and s_nop per round)
                     const uint4* thr = reinterpret_cast<const uint4*>(lds);
                     const uint32_t c1 = a.call_idx + t;
-                    const uint32_t g2 = (uint32_t)gid, g3 = ((uint32_t)(gid >> 32) & 0xFFFFFFu) | (STREAM_ENV << 24);
                     for (uint32_t sl = 0; sl < CH; sl += 4) {
                         uint32_t w[8];
-#pragma unroll
-                        for (uint32_t p = 0; p < 2; ++p) {
-                            uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
-                            asm volatile("" : "+s"(k0), "+s"(k1));
-                            w[4 * p] = ((used + sl) >> 1) + p;
-                            w[4 * p + 1] = c1;
-                            w[4 * p + 2] = g2;
-                            w[4 * p + 3] = g3;
-                            philox4x32_10(w + 4 * p, k0, k1);
-                        }
+                        philox_draw_sk(a.seed, (used + sl) >> 1, c1, gid, STREAM_ENV, w);
+                        philox_draw_sk(a.seed, ((used + sl) >> 1) + 1u, c1, gid, STREAM_ENV, w + 4);
                         uint32_t i[4];
                         uint4 t4[4];
 #pragma unroll
@@ -1350,7 +1368,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
                 for (uint32_t sl = 0; sl < CH; sl += 2) {
                     uint32_t w[4];
-                    philox_draw(a.seed, (used + sl) >> 1, a.call_idx + t, gid, STREAM_ENV, w);
+                    philox_draw_sk(a.seed, (used + sl) >> 1, a.call_idx + t, gid, STREAM_ENV, w);
 #pragma unroll
                     for (uint32_t h = 0; h < 2; ++h) {
                         const uint32_t i = philox_node<KIND>(w[2 * h], N);
@@ -1381,10 +1399,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         const uint32_t sp = nact > 1 ? __umulhi(k, magic) : k, r = k - sp * nact;
                         const uint4 cr = ctr_tab[r];
                         const uint32_t q = cr.w >> 24;
-                        uint32_t w[4] = {cr.x + sp, cr.y, cr.z, (cr.w & 0xFFFFFFu) | (STREAM_ENV << 24)};
-                        uint32_t k0s = (uint32_t)a.seed, k1s = (uint32_t)(a.seed >> 32);
-                        asm volatile("" : "+s"(k0s), "+s"(k1s));  // round keys by SALU adds (no spilled keys)
-                        philox4x32_10(w, k0s, k1s);
+                        uint32_t w[4];
+                        philox_draw_sk(a.seed, cr.x + sp, cr.y, (uint64_t)(cr.w & 0xFFFFFFu) << 32 | cr.z, STREAM_ENV, w);
                         const uint32_t i0 = philox_node<KIND>(w[0], N), i1 = philox_node<KIND>(w[2], N);
                         uint32_t j0, j1;
                         if constexpr (decltype(one_row)::value) {

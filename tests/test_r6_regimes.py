@@ -51,11 +51,17 @@ def G():
     return batch
 
 
-@pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step", "one_lane_per_step", "one_lane_fused"])
+@pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step", "one_lane_per_step", "one_lane_fused",
+                                  "per_step_chunk32", "fused_chunk32"])
 def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
+    """... and with either draw-round chunk (EnvArgs::chunk: 48 for these launches, 32 forced by
+    PBNSIM_ENV_CHUNK -- the chunk the host picks for long fused launches over large batches)."""
     import torch
 
     grp = "8" if mode.startswith("grp8") else "1"
+    chunk32 = mode.endswith("chunk32")
+    if chunk32:
+        monkeypatch.setenv("PBNSIM_ENV_CHUNK", "32")
     monkeypatch.setenv("PBNSIM_ENV_GROUP", grp)
     # every lane takes envs (lane mode proper), or one lane per wave (tail mode from the first env,
     # each wave taking its next env from the queue when one ends)
@@ -72,7 +78,7 @@ def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
                                 cfgd["reset_value"], seed=seed, env_base=base, reset_count=0)
     assert np.array_equal(b.get_state(), st)
     acts = _actions(np.random.default_rng(17), (T, B, A), net.n_nodes)
-    if mode.endswith("fused"):
+    if "fused" in mode:
         dev = torch.device("cuda", 0)
         d_a = torch.from_numpy(acts).to(dev)
         o_ = torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev)
@@ -90,6 +96,7 @@ def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
     assert info["env_grid"] == grid and info["env_lanes"] == int(grp)
     if grp == "1":
         assert info["env_kernel"] == 4 and info["env_lane_limit"] == (1 if mode.startswith("one_lane") else 64)
+        assert info["env_chunk"] == (32 if chunk32 else 48)
     capped = 0
     for t in range(T):
         ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=CAP)
