@@ -15,6 +15,13 @@ seeds and logs every launch's node updates. Per kernel configuration:
   effective_clock_GHz        = GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time (MI355X_MICROARCH.md
                                'DVFS give-back'; reads high on dispatches under ~0.3 ms)
 The first launch of each configuration is dropped (warm-up). Runs rocprofv3 as a CHILD process.
+
+`valu_pmc.py lds`: the same launches with LDS counters -> gpurun_out/r04_lds_pmc.json:
+  lds_insts_per_update       = SQ_INSTS_LDS / node updates (wave instructions)
+  bank_conflict_frac         = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles over all LDS-array
+                               cycles, MI355X_MICROARCH.md LDS)
+  lds_cycles_per_update      = SQ_LDS_IDX_ACTIVE / node updates
+  lds_issue_stall_frac       = SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES
 """
 import collections
 import csv
@@ -24,12 +31,16 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-COUNTERS = ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
-            "GRBM_GUI_ACTIVE"]
+SETS = {"valu": ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                 "GRBM_GUI_ACTIVE"],
+        "lds": ["SQ_INSTS_LDS", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+                "SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]}
+SET = sys.argv[1] if len(sys.argv) > 1 else "valu"
+COUNTERS = SETS[SET]
 
 
 def main():
-    outdir = ROOT / "gpurun_out" / "valu_pmc"
+    outdir = ROOT / "gpurun_out" / f"{SET}_pmc"
     cmd = ["rocprofv3", "--pmc", *COUNTERS, "--kernel-trace", "--output-format", "csv", "-d", str(outdir), "-o",
            "run", "--", sys.executable, str(ROOT / "tools" / "valu_pmc_child.py")]
     subprocess.run(cmd, check=True, cwd=str(ROOT))
@@ -58,6 +69,16 @@ def main():
         ups = sum(u for _, u in items)
         tot = {c: sum(d.get(c, 0.0) for d, _ in items) for c in COUNTERS}
         wall = sum(d["t"] for d, _ in items)
+        if SET == "lds":
+            res[key] = {"kernel": items[0][0]["name"], "launches": len(items), "node_updates": ups,
+                        "lds_insts_per_update": tot["SQ_INSTS_LDS"] / ups,
+                        "valu_wave_insts_per_update": tot["SQ_INSTS_VALU"] / ups,
+                        "bank_conflict_frac": tot["SQ_LDS_BANK_CONFLICT"] / max(tot["SQ_LDS_IDX_ACTIVE"], 1),
+                        "lds_cycles_per_update": tot["SQ_LDS_IDX_ACTIVE"] / ups,
+                        "lds_issue_stall_frac": tot["SQ_WAIT_INST_LDS"] / max(tot["SQ_WAVE_CYCLES"], 1),
+                        "profiled_kernel_s": sum(d["t"] for d, _ in items), "counters": tot,
+                        "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
+            continue
         res[key] = {"kernel": items[0][0]["name"], "launches": len(items), "node_updates": ups,
                     "valu_wave_insts_per_update": tot["SQ_INSTS_VALU"] / ups,
                     "valu_busy_frac": tot["SQ_ACTIVE_INST_VALU"] / max(tot["SQ_WAVE_CYCLES"], 1),
@@ -67,9 +88,9 @@ def main():
                     "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
     doc = {"kernels": res, "valu_peak": "256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s "
                                         "(MI355X_MICROARCH.md: chip parameters, wave scheduling)"}
-    (ROOT / "gpurun_out" / "r04_valu_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
-    print(json.dumps({k: {kk: v[kk] for kk in ("valu_wave_insts_per_update", "valu_busy_frac", "active_lane_frac",
-                                               "effective_clock_GHz", "launches")} for k, v in res.items()}))
+    (ROOT / "gpurun_out" / f"r04_{SET}_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
+    print(json.dumps({k: {kk: v for kk, v in r.items() if kk not in ("counters", "source", "kernel")}
+                      for k, r in res.items()}))
 
 
 if __name__ == "__main__":
