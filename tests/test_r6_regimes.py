@@ -311,6 +311,7 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
         n_ = torch.empty((T, B), dtype=torch.int32, device=dev)
         b.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, o_.data_ptr(), r_.data_ptr(), f_.data_ptr(),
                                    n_.data_ptr(), update_cap=cap)
+        b.sync()  # the launch is asynchronous on the batch's stream (env_handoffs syncs only with the hand-off on)
         handed.append(b.env_handoffs())
         got = [(o_[t].cpu().numpy().view(np.uint64), r_[t].cpu().numpy(), f_[t].cpu().numpy(),
                 n_[t].cpu().numpy().view(np.uint32)) for t in range(T)]
