@@ -1204,6 +1204,34 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint4 qb = erec_of(draw_idx(b));
                     return writers(qb, wround(qb));
                 };
+                // The next block's preparation in three stages placed between the current block's own, so
+                // each stage's LDS round trip (threshold row; env record; writer masks) is in flight while
+                // the current block computes (fixed point; prefix and commit) instead of stalling the wave
+                // ahead of them (one-row thresholds, one Philox call per lane): lone tail launch 57.9 -> 56.6 us,
+                // 131,072 envs per step at cap 2^20 2.11 -> 2.05 ms (profiles/r04_r6_tail_split_ab.json)
+#ifndef PBN_TAIL_NOSPLIT
+                constexpr bool SPLIT = ONE_ROW && !TAIL_PAIR;
+#else
+                constexpr bool SPLIT = false;
+#endif
+                struct StA {
+                    uint32_t ir, a32;
+                    uint4 t4;
+                };
+                auto stageA = [&](uint32_t b) {
+                    const uint32_t U = u0 + 64u * b + lane;
+                    uint32_t w4[4];
+                    draw(U >> 1, w4);
+                    const uint32_t odd = U & 1u;
+                    const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
+                    StA A;
+                    A.ir = __umul24(i, X.rs);
+                    asm volatile("" : "+v"(A.ir));
+                    A.a32 = odd ? w4[3] : w4[1];
+                    A.t4 = reinterpret_cast<const uint4*>(lds)[i];
+                    return A;
+                };
+                auto stageB = [&](const StA& A) { return erec[(A.ir + cnt4(A.t4, A.a32)) & 0xFFFFu]; };
                 TailDraw D = prepare(0u);
 #ifdef PBN_STAMPS
                 const uint64_t sess_rt = __builtin_amdgcn_s_memrealtime();
@@ -1227,7 +1255,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint32_t b1 = *reinterpret_cast<const uint32_t*>(colb + (q.x >> 16));
                     const uint32_t b2 = *reinterpret_cast<const uint32_t*>(colb + (q.y & 0xFFFFu));
                     const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + (q.y >> 16));
-                    const TailDraw Dn = prepare(k + 1u);  // while those reads are in flight
+                    [[maybe_unused]] StA An;
+                    [[maybe_unused]] TailDraw Dn;
+                    if constexpr (SPLIT)
+                        An = stageA(k + 1u);  // while those reads are in flight
+                    else
+                        Dn = prepare(k + 1u);
 #ifdef PBN_STAMPS
                     const uint64_t c_prep = __builtin_amdgcn_s_memtime();
 #endif
@@ -1259,6 +1292,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         yn = fround(y);
                     }
                     y = yn;
+                    [[maybe_unused]] uint4 qn;
+                    if constexpr (SPLIT) qn = stageB(An);
 #ifdef PBN_STAMPS
                     const uint64_t c_fp = __builtin_amdgcn_s_memtime();
 #endif
@@ -1277,7 +1312,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     u += nd;
                     hitf = SM != 0ull;
                     fin = hitf || u >= a.update_cap;
-                    D = Dn;  // (the commit above and the next block's plane reads stay in issue order)
+                    if constexpr (SPLIT)
+                        D = writers(qn, wround(qn));
+                    else
+                        D = Dn;  // (the commit above and the next block's plane reads stay in issue order)
 #ifdef PBN_STAMPS
                     {
                         const uint64_t c_end = __builtin_amdgcn_s_memtime();
