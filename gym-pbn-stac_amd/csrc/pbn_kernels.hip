@@ -1430,8 +1430,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // k / nact as a multiply-high by ceil(2^32 / nact): exact for k < 2^16 (nact == 1 handled apart,
             // its multiplier 2^32 does not fit 32 bits)
             const uint32_t magic = kRankMagic.v[nact];  // a 64-bit divide here was ~120 scalar instructions
-            auto rounds = [&](auto one_row) {
-                for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+            auto rounds = [&](auto one_row, uint32_t kstart) {
+                for (uint32_t k0 = kstart; k0 < total; k0 += 64) {
                     const uint32_t k = k0 + lane;
                     if (k < total) {
                         const uint32_t sp = nact > 1 ? __umulhi(k, magic) : k, r = k - sp * nact;
@@ -1457,10 +1457,51 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                 }
             };
+#ifndef PBN_ROUNDS_SINGLE
+            // one-row thresholds: two rounds per iteration, their counter entries and then their four rows
+            // read together, so each LDS wait serves two rounds (a round waited twice: entry, then rows)
+            auto rounds2 = [&]() {
+                const uint4* thr = reinterpret_cast<const uint4*>(lds);
+                uint32_t k0 = 0;
+                for (; k0 + 64u < total; k0 += 128) {  // (a last lone round goes to the one-round loop)
+                    const uint32_t ka = k0 + lane, kb = ka + 64u;
+                    const bool va = ka < total, vb = kb < total;
+                    const uint32_t kac = va ? ka : 0u, kbc = vb ? kb : 0u;  // clamped: reads stay in the table
+                    const uint32_t spa = nact > 1 ? __umulhi(kac, magic) : kac, ra = kac - spa * nact;
+                    const uint32_t spb = nact > 1 ? __umulhi(kbc, magic) : kbc, rb = kbc - spb * nact;
+                    const uint4 ca = ctr_tab[ra], cb = ctr_tab[rb];
+                    uint32_t wa[4], wb[4];
+                    philox_draw_sk(a.seed, ca.x + spa, ca.y, (uint64_t)(ca.w & 0xFFFFFFu) << 32 | ca.z, STREAM_ENV, wa);
+                    philox_draw_sk(a.seed, cb.x + spb, cb.y, (uint64_t)(cb.w & 0xFFFFFFu) << 32 | cb.z, STREAM_ENV, wb);
+                    const uint32_t ia0 = philox_node<KIND>(wa[0], N), ia1 = philox_node<KIND>(wa[2], N);
+                    const uint32_t ib0 = philox_node<KIND>(wb[0], N), ib1 = philox_node<KIND>(wb[2], N);
+                    const uint4 ta0 = thr[ia0], ta1 = thr[ia1], tb0 = thr[ib0], tb1 = thr[ib1];
+                    uint32_t ra0 = __umul24(ia0, X.rs), ra1 = __umul24(ia1, X.rs);
+                    uint32_t rb0 = __umul24(ib0, X.rs), rb1 = __umul24(ib1, X.rs);
+                    asm volatile("" : "+v"(ra0), "+v"(ra1), "+v"(rb0), "+v"(rb1));
+                    if (va) {
+                        const uint32_t q = ca.w >> 24;
+                        gbuf[(2 * spa) * 64 + q] = (uint16_t)(ra0 + cnt4(ta0, wa[1]));
+                        gbuf[(2 * spa + 1) * 64 + q] = (uint16_t)(ra1 + cnt4(ta1, wa[3]));
+                    }
+                    if (vb) {
+                        const uint32_t q = cb.w >> 24;
+                        gbuf[(2 * spb) * 64 + q] = (uint16_t)(rb0 + cnt4(tb0, wb[1]));
+                        gbuf[(2 * spb + 1) * 64 + q] = (uint16_t)(rb1 + cnt4(tb1, wb[3]));
+                    }
+                }
+                rounds(std::true_type{}, k0);
+            };
             if (X.tp4 == 4u)
-                rounds(std::true_type{});
+                rounds2();
             else
-                rounds(std::false_type{});
+                rounds(std::false_type{}, 0u);
+#else
+            if (X.tp4 == 4u)
+                rounds(std::true_type{}, 0u);
+            else
+                rounds(std::false_type{}, 0u);
+#endif
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
