@@ -374,7 +374,8 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
     GLOBAL env id and env step (SURVEY §8(d)), so the global batch is one workload at any GPU count;
     attractors ``spec`` (r6_attractors); update cap ``cap``. Timed twice: one launch per env step
     (closed loop), then one launch per chunk (actions known for it). Every timed chunk reports its
-    kernel time (HIP events), the slowest env's updates and (fused) the tail hand-offs of its launch;
+    kernel time (HIP events, read after the timed window) and the slowest env's updates; the last fused
+    launch's tail hand-offs are reported once;
     with ``check`` the fused run's last chunk is checked on sampled global ids (r6_shard_check)."""
     import torch
 
@@ -404,6 +405,8 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
         col = TrajectoryCollector(b, cfg, T, A, dev, update_cap=cap, dist=dist if gather else None, fused=fused)
 
         def chunks(diag=None):
+            # nothing is read back to the host inside the loop: the per-chunk figures stay on
+            # the device (slowest env) or in the batch's event pairs (kernel ms), read after the window
             ups = torch.zeros((), dtype=torch.int64, device=dev)
             stats = []
             for _ in range(n_chunks):
@@ -411,15 +414,16 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
                 u, st = chunk_stats(buf)
                 ups += u
                 stats.append(st)
-                if diag is not None:  # the collector synced the batch stream after the chunk
-                    kms_c, nl = b.timing_read()  # this chunk's launches (HIP events), then reset
-                    d = {"kernel_ms": kms_c, "launches": nl,
-                         # the env whose T env steps took the most updates: a fused chunk ends with it
-                         "slowest_env_updates": int(buf["n_updates"].to(torch.int64).sum(dim=0).max().item())}
-                    if fused:
-                        d["handoffs"] = b.env_handoffs()  # tail envs passed between the waves of a workgroup
-                    diag.append(d)
+                if diag is not None:  # the env whose T env steps took the most updates: a fused chunk ends with it
+                    diag.append(buf["n_updates"].to(torch.int64).sum(dim=0).max())
             return buf, ups, stats
+
+        def diag_after(slowest):
+            # every chunk issues the same launches: the per-launch kernel times split evenly into chunks
+            each = b.timing_read_each()
+            per = max(len(each) // max(n_chunks, 1), 1)
+            return [{"kernel_ms": float(sum(each[k * per:(k + 1) * per])), "launches": per,
+                     "slowest_env_updates": int(x.item())} for k, x in enumerate(slowest)]
 
         # warm-up: the timed loop itself, untimed, with the per-launch events on -- the first use
         # of the events (created on demand, then reused) and of torch's small kernels costs tens
@@ -440,6 +444,7 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
         if dist is not None:
             dist.barrier()
         dt = max_over_ranks(time.perf_counter() - t0, dist, device=dev)
+        diag = diag_after(diag)
         b.timing(0)
         kms = sum(d["kernel_ms"] for d in diag)
         local_ups = float(ups.item())
@@ -457,6 +462,7 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
     b.close()
     b, buf, dt, ups, tail, k_fused, diag = run(True)
     lanes = b.info()["env_lanes"]
+    handoffs = b.env_handoffs()  # the last fused launch's tail envs passed between the waves of a workgroup
     out = {"unit": "env-steps/s", "attractors": spec, "attractors_desc": desc, "update_cap": cap,
            "value": world * B * T * n_chunks / dt, "node_updates_per_s": ups / dt,
            "launch": "one per chunk (T env steps per env in one launch; actions known for the chunk)",
@@ -467,6 +473,7 @@ def r6_figure(args, world, rank, device, dist, valu, spec, cap, n_chunks, gather
            "chunks": n_chunks, "s_per_chunk": dt / n_chunks, "tail": tail,
            "tail_one_launch_per_env_step": tail_step,
            "chunk_diag": diag, "chunk_diag_one_launch_per_env_step": diag_step,
+           "handoffs_last_fused_launch": handoffs,
            "chunk_bytes_per_gpu": sum(t.numel() * t.element_size() for t in buf.values())}
     for key, (ks, nu), name in ((f"k_env:bittner199:{B}:fused{T}", k_fused, "roofline"),
                                 (f"k_env:bittner199:{B}:per_step", k_step, "roofline_one_launch_per_env_step")):

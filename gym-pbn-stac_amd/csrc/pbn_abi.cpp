@@ -173,6 +173,7 @@ struct pbn_batch {
     int env_tail = -1;        // PBNSIM_ENV_TAIL: the R6 kernel's tail-mode threshold (live envs per wave), -1 = default
     int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
     bool env_steal = true;    // PBNSIM_ENV_STEAL=0: no hand-off of tail envs between a workgroup's waves (k_env, mode 4)
+    bool env_kernel_image = false;  // PBNSIM_ENV_KERNEL_IMAGE=1: k_env builds its LDS image (no host-built image)
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
@@ -530,6 +531,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_TAIL")) b->env_tail = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_LANES")) b->env_lane_limit = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_STEAL")) b->env_steal = atoi(v) != 0;
+    if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -1429,10 +1431,14 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
             mode = cfg->fast;  // too large for the u16 record index / one workgroup's LDS
         else if (cfg->H <= 4)
             mode = 4;  // the same kernel with one packed counter word (<= 4 cubes)
+        // mode 4 adds the workgroup hand-off control words: re-check the fit with the final mode
+        if (mode == 4 && env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 4, 1, 0, ENV_CHUNK_SMALL) > 64u * 1024u)
+            mode = cfg->fast;
     }
     if (mode != 2 && mode != 4) erec_shift = 0;
     const void* gen_img = nullptr;
-    if ((mode == 2 || mode == 4) && (cfg->L.bytes + erec_shift) % 16u == 0u) {
+    // PBNSIM_ENV_KERNEL_IMAGE=1: the kernel builds its LDS image itself (tests keep that path covered)
+    if ((mode == 2 || mode == 4) && (cfg->L.bytes + erec_shift) % 16u == 0u && !b->env_kernel_image) {
         std::lock_guard<std::mutex> g(cfg->mu);
         if (cfg->gen_image.empty()) cfg->gen_image = env_gen_image(cfg, erec_shift);
         auto& d = cfg->dev[b->device];  // on() above created it
@@ -1724,6 +1730,21 @@ int pbn_env_handoffs(pbn_batch* b, uint32_t* count) {
     if (!b->steal_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
     HIP_TRY(hipMemcpy(count, b->s_steal.p, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int pbn_timing_read_each(pbn_batch* b, double* ms_each, uint64_t cap, uint64_t* launches) {
+    CHECK_NN(b, "batch");
+    if (b->timing == 2 || b->region_closed) return fail(PBN_E_INVALID, "per-launch times need timing mode 1");
+    SET_DEV(b);
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    for (size_t k = 0; k < b->ev_used && k < cap; k++) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev_pool[k].first, b->ev_pool[k].second));
+        if (ms_each) ms_each[k] = ms;
+    }
+    if (launches) *launches = b->ev_used;
+    b->ev_used = 0;
     return 0;
 }
 

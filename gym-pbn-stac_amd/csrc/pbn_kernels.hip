@@ -258,33 +258,6 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
         for (int k = 0; k < W; ++k) out[k] = s[k] ^ ((uint32_t)k == wi ? m : 0ull);
         store_state<W>(a.state + eh * W, out);
     };
-#ifdef PBN_STEP_REGSEL
-    // Measurement variant: the four operand bits picked from the env's words in
-    // registers (word select by the node's word index, 64-bit shift), no plane writes; the selects'
-    // conditions depend on the record only, so they can be formed before the state lands
-    (void)eval;
-    auto bit_of = [&](const uint64_t (&s)[W], uint32_t n) -> uint32_t {
-        const uint32_t k = n >> 6;
-        uint64_t w = s[0];
-#pragma unroll
-        for (int q = 1; q < W; ++q) w = (k == (uint32_t)q) ? s[q] : w;
-        return (uint32_t)(w >> (n & 63u)) & 1u;
-    };
-    auto eval_r = [&](const uint64_t (&s)[W], uint32_t i, uint64_t r, uint32_t& own) {
-        own = bit_of(s, i);
-        const uint32_t p = (bit_of(s, (uint32_t)r & 0xFFFFu) << 3) | (bit_of(s, (uint32_t)(r >> 16) & 0xFFFFu) << 2) |
-                           (bit_of(s, (uint32_t)(r >> 32) & 0xFFFFu) << 1) | own;
-        return (uint32_t)(r >> (48 + p)) & 1u;
-    };
-    uint32_t own0, own1;
-    const uint32_t y0 = eval_r(cur, i0, r0, own0);
-#pragma unroll
-    for (int k = 0; k < W; ++k) asm volatile("" ::"v"(nxt[k]));
-    if (e < a.B && own0 != y0) put(cur, e, i0);
-    const uint32_t y1 = eval_r(nxt, i1, r1, own1);
-    if (e1 < a.B && own1 != y1) put(nxt, e1, i1);
-    (void)P;
-#else
     uint32_t self0, self1;
     const uint32_t y0 = eval(cur, i0, r0, self0);
     // env 0 is stored before env 1 is evaluated; env 1's loads (issued right behind env 0's) are waited
@@ -294,7 +267,6 @@ __device__ __forceinline__ void k_step_pair(const StepArgs& a, uint8_t* lds, uin
     if (e < a.B && ((self0 >> (i0 & 31u)) & 1u) != y0) put(cur, e, i0);
     const uint32_t y1 = eval(nxt, i1, r1, self1);  // past B: junk from a clamped load, never stored
     if (e1 < a.B && ((self1 >> (i1 & 31u)) & 1u) != y1) put(nxt, e1, i1);
-#endif
 }
 
 // Step mode (T == 1, Philox; REPLAY == 0) and replay mode (REPLAY == 1: T updates from the
@@ -610,8 +582,8 @@ __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01
 #ifndef PBN_ENV_OWN_DRAWS_MIN
 #define PBN_ENV_OWN_DRAWS_MIN 40  // measurement builds (tools/build_exp.sh) change this
 #endif
-constexpr uint32_t ENV_OWN_DRAWS_MIN = PBN_ENV_OWN_DRAWS_MIN;
-constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many updates are resolved longest-first  // active lanes from which a wave skips the shared draw tables
+constexpr uint32_t ENV_OWN_DRAWS_MIN = PBN_ENV_OWN_DRAWS_MIN;  // active lanes from which a wave skips the shared draw tables
+constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many updates are resolved longest-first
 
 // ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
 struct RankMagic {
@@ -782,7 +754,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 while (idle != 0u && n != 0u) {
                     const uint32_t w = (uint32_t)__ffs(idle) - 1u, bit = 1u << w;
                     idle &= ~bit;
-                    if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
+                    // acquire: the claimed wave cleared its flag before setting its idle bit (release), so
+                    // the flag / box writes below are ordered after that clear
+                    if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
                         claimed |= bit;
                         --n;
                     }
@@ -1039,11 +1013,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // needs <= 16 predictors per node), as guarded straight-line reads rather than a loop
                 const uint32_t nq = X.tp4 >> 2;
                 auto tail_session = [&](auto one_row) {
-#ifdef PBN_TAIL_PAIR
-                constexpr bool TAIL_PAIR = true;
-#else
-                constexpr bool TAIL_PAIR = false;  // one Philox call per lane per block, no ds_bpermute round trip
-#endif
                 // one_row: every node's thresholds fit one 16-B row (<= 5 predictors: Bittner-200), so a
                 // choice is one ds_read_b128 and the two choices of a Philox pair issue back to back
                 constexpr bool ONE_ROW = decltype(one_row)::value;
@@ -1100,12 +1069,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                 };
                 // Draws. STREAM_ENV: update U of the env step takes Philox call U >> 1, words 2(U & 1) and
-                // 2(U & 1) + 1, so two blocks [ub, ub + 128) need 64 calls: lane k makes call (ub >> 1) + k
-                // once per pair of blocks and keeps both of its updates' env-record indices (u16 each);
-                // the pair's first block takes lane (k >> 1)'s, the second lane 32 + (k >> 1)'s, one
-                // ds_bpermute per block -- half the Philox work of one call per lane per block. A session
-                // starts at an even update (a lane-mode chunk boundary, CH updates, or 0) and
-                // advances 64 per block; an odd start draws per lane (not expected).
+                // 2(U & 1) + 1: lane k of the block starting at update ub makes call (ub + k) >> 1 and uses
+                // its update's half (one call per lane per block; pairing two blocks' calls over a
+                // ds_bpermute measured no faster, profiles/r04_r6_tail_philox_split_ab.json,
+                // tools/patches/r04_variants.patch).
                 // The next block is prepared (draw, record, writer round) while the current one resolves;
                 // it is speculative (dropped when the current block ends the env step; the writer table is
                 // cleared in the same round that sets it, so it is all zero whenever a session ends).
@@ -1113,39 +1080,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // k + 3's draw issued while k resolves): a lone chain 0.0156 vs 0.0155 us per update, and
                 // 2-5 more VGPRs spilled in the lane-mode path (the kernel is at its 128-VGPR bound).
                 const uint32_t u0 = u;
-                uint32_t epair = 0u;
-                const uint32_t pick_addr = (lane >> 1) * 4u, pick_sh = (lane & 1u) * 16u;
-                auto draw_idx = [&](uint32_t b) -> uint32_t {  // block b's env-record index, << pick_sh
-                    const uint32_t ub = u0 + 64u * b;
-                    if (!TAIL_PAIR || (u0 & 1u)) {
-                        const uint32_t U = ub + lane;
-                        uint32_t w4[4];
-                        draw(U >> 1, w4);
-                        const uint32_t odd = U & 1u;
-                        const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
-                        uint32_t ir = __umul24(i, X.rs);
-                        asm volatile("" : "+v"(ir));  // else folded with the choice into a quarter-rate v_mad_u64_u32
-                        return (ir + choice(i, odd ? w4[3] : w4[1])) << pick_sh;
-                    }
-                    if (!(b & 1u)) {
-                        uint32_t w4[4];
-                        draw((ub >> 1) + lane, w4);
-                        const uint32_t i0 = philox_node<KIND>(w4[0], N), i1 = philox_node<KIND>(w4[2], N);
-                        uint32_t j0, j1;
-                        if constexpr (ONE_ROW) {  // both rows read before either is compared
-                            const uint4 t0 = reinterpret_cast<const uint4*>(lds)[i0];
-                            const uint4 t1 = reinterpret_cast<const uint4*>(lds)[i1];
-                            j0 = cnt4(t0, w4[1]);
-                            j1 = cnt4(t1, w4[3]);
-                        } else {
-                            j0 = choice(i0, w4[1]);
-                            j1 = choice(i1, w4[3]);
-                        }
-                        epair = (__umul24(i0, X.rs) + j0) | ((__umul24(i1, X.rs) + j1) << 16);
-                    }
-                    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pick_addr + (b & 1u) * 128u), (int)epair);
+                auto draw_idx = [&](uint32_t b) -> uint32_t {  // block b's env-record index
+                    const uint32_t U = u0 + 64u * b + lane;
+                    uint32_t w4[4];
+                    draw(U >> 1, w4);
+                    const uint32_t odd = U & 1u;
+                    const uint32_t i = philox_node<KIND>(odd ? w4[2] : w4[0], N);
+                    uint32_t ir = __umul24(i, X.rs);
+                    asm volatile("" : "+v"(ir));  // else folded with the choice into a quarter-rate v_mad_u64_u32
+                    return ir + choice(i, odd ? w4[3] : w4[1]);
                 };
-                auto erec_of = [&](uint32_t E) { return erec[(E >> pick_sh) & 0xFFFFu]; };
+                auto erec_of = [&](uint32_t E) { return erec[E & 0xFFFFu]; };
                 // Writer round of a block (its records q): node n's 64-bit writer mask at wmc + 8n, n = plane
                 // offset / 32 | bit (offset = dword * 1024); or, read the four operands' masks, clear.
                 struct WRound {
@@ -1209,11 +1154,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // the current block computes (fixed point; prefix and commit) instead of stalling the wave
                 // ahead of them (one-row thresholds, one Philox call per lane): lone tail launch 57.9 -> 56.6 us,
                 // 131,072 envs per step at cap 2^20 2.11 -> 2.05 ms (profiles/r04_r6_tail_split_ab.json)
-#ifndef PBN_TAIL_NOSPLIT
-                constexpr bool SPLIT = ONE_ROW && !TAIL_PAIR;
-#else
-                constexpr bool SPLIT = false;
-#endif
+                constexpr bool SPLIT = ONE_ROW;
                 struct StA {
                     uint32_t ir, a32;
                     uint4 t4;
@@ -1375,7 +1316,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // round costs two dependent LDS round trips more)
                 // (a chunk starts at an even update index: one Philox call per pair of updates)
                 const uint64_t gid = a.env_base + (uint64_t)e;
-#ifndef PBN_GEN_GENERIC
                 if (X.tp4 == 4u) {
                     // one threshold row per node (<= 5 predictors: Bittner-200): four updates (two Philox
                     // calls) per iteration with their four 16-B rows read back to back, so one LDS wait
@@ -1403,7 +1343,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         }
                     }
                 } else
-#endif
                 for (uint32_t sl = 0; sl < CH; sl += 2) {
                     uint32_t w[4];
                     philox_draw_sk(a.seed, (used + sl) >> 1, a.call_idx + t, gid, STREAM_ENV, w);
@@ -1457,7 +1396,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                 }
             };
-#ifndef PBN_ROUNDS_SINGLE
             // one-row thresholds: two rounds per iteration, their counter entries and then their four rows
             // read together, so each LDS wait serves two rounds (a round waited twice: entry, then rows)
             auto rounds2 = [&]() {
@@ -1496,12 +1434,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 rounds2();
             else
                 rounds(std::false_type{}, 0u);
-#else
-            if (X.tp4 == 4u)
-                rounds(std::true_type{}, 0u);
-            else
-                rounds(std::false_type{}, 0u);
-#endif
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();

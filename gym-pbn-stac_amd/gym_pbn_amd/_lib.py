@@ -124,6 +124,7 @@ SIGNATURES = {
     "pbn_synch_step": (C.c_int, [_vp, C.c_uint32, _u32p]),
     "pbn_timing_enable": (C.c_int, [_vp, C.c_int]),
     "pbn_timing_read": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "pbn_timing_read_each": (C.c_int, [_vp, C.POINTER(C.c_double), C.c_uint64, C.POINTER(C.c_uint64)]),
     "pbn_env_handoffs": (C.c_int, [_vp, _u32p]),
 }
 

@@ -398,6 +398,13 @@ class PBNBatch:
         L.check(L.lib.pbn_timing_read(self._h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def timing_read_each(self, cap: int = 1 << 16):
+        """Timing mode 1: every timed launch's kernel ms since the last read, in launch order."""
+        buf = (C.c_double * cap)()
+        n = C.c_uint64(0)
+        L.check(L.lib.pbn_timing_read_each(self._h, buf, cap, C.byref(n)))
+        return [buf[k] for k in range(min(n.value, cap))]
+
     def env_handoffs(self) -> int:
         """Envs the last R6 launch handed from tail-mode waves to idle ones (0 with the hand-off off)."""
         n = C.c_uint32(0)

@@ -247,6 +247,10 @@ int pbn_ssd_run(pbn_batch *b, const int32_t *target_nodes, int n_targets, const 
  *      mode 2: one region from before the first launch to after the last (launch gaps included) ---- */
 int pbn_timing_enable(pbn_batch *b, int enable);
 int pbn_timing_read(pbn_batch *b, double *kernel_ms, uint64_t *launches); /* syncs, then resets */
+/* mode 1 only: each timed launch's kernel ms in launch order (up to cap; *launches = how many were timed);
+ * syncs, then resets like pbn_timing_read. Lets a timed loop keep per-launch figures without host reads
+ * inside it. */
+int pbn_timing_read_each(pbn_batch *b, double *ms_each, uint64_t cap, uint64_t *launches);
 /* Envs handed from a tail-mode wave to an idle one during the last R6 env-step launch (env_kernel 4;
  * 0 when the hand-off was off). Syncs the batch stream. Diagnostics: the reference has no counterpart
  * (its until-attractor loop, pbn_target_multi.py:135-146, runs one env in one process). */

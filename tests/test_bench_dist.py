@@ -48,6 +48,12 @@ class _FakeBatch:
     def timing_read(self):
         return 0.01 * max(self._launches, 1), max(self._launches, 1)
 
+    def timing_read_each(self):
+        return [0.01] * max(self._launches, 1)
+
+    def env_handoffs(self):
+        return 0
+
     def info(self):
         return {"env_lanes": 1, "roll_lanes": 1}
 
@@ -139,7 +145,8 @@ def test_two_rank_bench_bookkeeping_on_cpu(tmp_path):
     sc = d["shard_check"]
     assert sc["ranks"] == 2 and sc["match"] is True and sc["sampled_env_pairs"] == 32
     assert r6["shard_check"]["ranks"] == 2 and r6["shard_check"]["sampled_env_pairs"] == 16
-    assert len(r6["chunk_diag"]) == 2 and "handoffs" in r6["chunk_diag"][0]
+    assert len(r6["chunk_diag"]) == 2 and "slowest_env_updates" in r6["chunk_diag"][0]
+    assert "handoffs_last_fused_launch" in r6
     assert "process_census" in d
 
 

@@ -52,11 +52,16 @@ def G():
 
 
 @pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step", "one_lane_per_step", "one_lane_fused",
-                                  "per_step_chunk32", "fused_chunk32"])
+                                  "per_step_chunk32", "fused_chunk32", "per_step_kernel_image"])
 def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
     """... and with either draw-round chunk (EnvArgs::chunk: 48 for these launches, 32 forced by
-    PBNSIM_ENV_CHUNK -- the chunk the host picks for long fused launches over large batches)."""
+    PBNSIM_ENV_CHUNK -- the chunk the host picks for long fused launches over large batches); and with
+    the kernel building its LDS image itself (PBNSIM_ENV_KERNEL_IMAGE=1) instead of staging the
+    host-built one (pbn_abi.cpp env_gen_image), so both constructions stay exact."""
     import torch
+
+    if mode.endswith("kernel_image"):
+        monkeypatch.setenv("PBNSIM_ENV_KERNEL_IMAGE", "1")
 
     grp = "8" if mode.startswith("grp8") else "1"
     chunk32 = mode.endswith("chunk32")
@@ -329,6 +334,86 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
         import warnings    # wave scheduling: a diagnostic, not a correctness condition
 
         warnings.warn(f"no tail hand-off happened in this run ({handed}); exactness still checked below")
+    for t in range(T):
+        ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=cap)
+        obs, rew, flags, nup = got[t]
+        assert np.array_equal(nup, ref["n_updates"]), t
+        assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), t
+        assert np.array_equal(flags, ref["flags"]), t
+        st, ns = ref["state"], ref["n_steps"]
+    assert np.array_equal(b.get_state(), st) and np.array_equal(b.get_n_steps(), ns)
+    b.close()
+
+
+@pytest.mark.parametrize("mode", ["per_step", "fused"])
+def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypatch, mode):
+    """A case in which the workgroup hand-off must happen: one workgroup (4 waves), two
+    lanes per wave taking envs, 6 envs -- three waves hold two envs each, the fourth none and goes idle
+    at once. Every env's first env step is long (its action row is chosen with the oracle so that
+    each runs >= 2,048 updates: per env, action rows are tried on the oracle until one does), so a wave resolving its first env reaches its 16-block re-check
+    (tail_session: every 16 blocks) with its second env unstarted while the idle wave waits: the
+    hand-off happens (asserted), and every output equals the oracle."""
+    import torch
+
+    monkeypatch.setenv("PBNSIM_ENV_LANES", "2")
+    monkeypatch.setenv("PBNSIM_ENV_GRID", "1")
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    net = load_network("bittner199")
+    gnet = G.Net(net)
+    atts, _ = bench.r6_attractors("fixture", net.n_nodes)
+    cfg = G.EnvConfig(gnet, atts, horizon=100)
+    cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
+                horizon=100)
+    o = oracle_mod.Oracle(net)
+    B, seed, base, T, A, cap = 6, 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
+                                cfg.reset_value, seed=seed, env_base=base, reset_count=0)
+    # per env, the first candidate action row (oracle) whose first env step runs >= 2,048 updates
+    acts = _actions(np.random.default_rng(77), (T, B, A), net.n_nodes)
+    rng = np.random.default_rng(78)
+    need = np.ones(B, bool)
+    for _ in range(400):
+        cand = _actions(rng, (B, A), net.n_nodes)
+        r = o.env_step_multi(cfgd, st, ns, cand, seed=seed, env_base=base, call_idx=0, update_cap=cap)
+        ok = need & (r["n_updates"] >= 2048)
+        acts[0][ok] = cand[ok]
+        need &= ~ok
+        if not need.any():
+            break
+    assert not need.any()
+    b = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
+    b.env_reset(cfg)
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
+                                cfg.reset_value, seed=seed, env_base=base, reset_count=0)
+    assert np.array_equal(b.get_state(), st)
+    handed = []
+    if mode == "fused":
+        dev = torch.device("cuda", 0)
+        d_a = torch.from_numpy(acts).to(dev)
+        o_ = torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev)
+        r_ = torch.empty((T, B), dtype=torch.int32, device=dev)
+        f_ = torch.empty((T, B), dtype=torch.uint8, device=dev)
+        n_ = torch.empty((T, B), dtype=torch.int32, device=dev)
+        b.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, o_.data_ptr(), r_.data_ptr(), f_.data_ptr(),
+                                   n_.data_ptr(), update_cap=cap)
+        b.sync()
+        handed.append(b.env_handoffs())
+        got = [(o_[t].cpu().numpy().view(np.uint64), r_[t].cpu().numpy(), f_[t].cpu().numpy(),
+                n_[t].cpu().numpy().view(np.uint32)) for t in range(T)]
+    else:
+        got = []
+        for t in range(T):
+            got.append(b.env_step_multi(cfg, acts[t], update_cap=cap))
+            handed.append(b.env_handoffs())
+    info = b.info()
+    assert info["env_kernel"] == 4 and info["env_lane_limit"] == 2 and info["env_grid"] == 1
+    assert info["env_handoff"] == 1
+    assert handed[0] > 0, handed  # the first launch (every env long) must hand off
     for t in range(T):
         ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=cap)
         obs, rew, flags, nup = got[t]

@@ -17,7 +17,7 @@ namespace {
 
 __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64_t B, uint32_t write_pct,
                                                 uint32_t passes, uint64_t* __restrict__ sink, uint32_t salt,
-                                                uint32_t glog) {
+                                                uint32_t glog, uint32_t wbytes) {
     const uint64_t stride = (uint64_t)gridDim.x * 1024u;
     uint64_t acc = 0;
     for (uint32_t p = 0; p < passes; ++p) {
@@ -37,17 +37,28 @@ __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64
             acc ^= a0.x ^ a1.y;
             // a fixed subset of envs is written (write_pct %), as the dirty-store kernel writes
             // the envs whose updated bit changed
+            // wbytes: 32 = the whole env (the kernel's store), 16 = the half holding the changed word,
+            // 8 = only the changed word (word index from the env id, as the updated node's word varies)
+            auto wr = [&](ulonglong2* q, uint64_t e, ulonglong2 v0, ulonglong2 v1) {
+                const uint32_t wsel = (uint32_t)((e * 0x9E3779B97F4A7C15ull) >> 62);
+                if (wbytes >= 32u) {
+                    q[0] = v0;
+                    q[1] = v1;
+                } else if (wbytes == 16u) {
+                    q[wsel >> 1] = (wsel >> 1) ? v1 : v0;
+                } else {
+                    reinterpret_cast<uint64_t*>(q)[wsel] = v0.x ^ v1.y ^ wsel;
+                }
+            };
             if ((uint32_t)((((ea >> glog) ^ salt) * 2654435761u) >> 7) % 100u < write_pct) {
                 a0.x += 1;
-                qa[0] = a0;
-                qa[1] = a1;
+                wr(qa, ea, a0, a1);
             }
             if (hb) {
                 acc ^= b0.x ^ b1.y;
                 if ((uint32_t)((((eb >> glog) ^ salt) * 2654435761u) >> 7) % 100u < write_pct) {
                     b0.x += 1;
-                    qb[0] = b0;
-                    qb[1] = b1;
+                    wr(qb, eb, b0, b1);
                 }
             }
         }
@@ -61,7 +72,7 @@ __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64
 // fraction, `passes` passes per launch and `launches` timed launches (after 3 untimed ones).
 // Returns 0 on success, a HIP error code otherwise.
 static int probe_impl(uint64_t n_envs, int write_pct, int passes, int launches, int vary, int glog,
-                      double* us_per_pass) {
+                      double* us_per_pass, int wbytes = 32) {
     if (!us_per_pass || n_envs < 2048 || passes < 1 || launches < 1) return -1;
     int dev = 0, n_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -2;
@@ -80,14 +91,15 @@ static int probe_impl(uint64_t n_envs, int write_pct, int passes, int launches, 
     if (e == hipSuccess) {
         for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(k_probe, dim3(grid), dim3(1024), 0, 0, s, n_envs,
                                                        (uint32_t)write_pct, (uint32_t)passes, sink,
-                                                       vary ? (uint32_t)(w * 0x9E3779B1u) : 0u, (uint32_t)glog);
+                                                       vary ? (uint32_t)(w * 0x9E3779B1u) : 0u, (uint32_t)glog,
+                                                       (uint32_t)wbytes);
         e = hipEventRecord(t0, 0);
     }
     if (e == hipSuccess) {
         for (int k = 0; k < launches; ++k)
             hipLaunchKernelGGL(k_probe, dim3(grid), dim3(1024), 0, 0, s, n_envs, (uint32_t)write_pct,
                                (uint32_t)passes, sink, vary ? (uint32_t)((k + 3) * 0x9E3779B1u) : 0u,
-                               (uint32_t)glog);
+                               (uint32_t)glog, (uint32_t)wbytes);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipEventRecord(t1, 0);
@@ -114,4 +126,10 @@ extern "C" int mall_probe_vary(uint64_t n_envs, int write_pct, int passes, int l
 // Written envs decided per aligned group of 2^glog envs (all or none), drawn afresh per launch.
 extern "C" int mall_probe_group(uint64_t n_envs, int write_pct, int glog, int launches, double* us_per_pass) {
     return probe_impl(n_envs, write_pct, 1, launches, 1, glog, us_per_pass);
+}
+
+// The vary pattern with only wbytes (8, 16 or 32) of each written env stored.
+extern "C" int mall_probe_wbytes(uint64_t n_envs, int write_pct, int wbytes, int launches, double* us_per_pass) {
+    if (wbytes != 8 && wbytes != 16 && wbytes != 32) return -1;
+    return probe_impl(n_envs, write_pct, 1, launches, 1, 0, us_per_pass, wbytes);
 }
