@@ -174,6 +174,7 @@ struct pbn_batch {
     int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
     bool env_steal = true;    // PBNSIM_ENV_STEAL=0: no hand-off of tail envs between a workgroup's waves (k_env, mode 4)
     bool env_kernel_image = false;  // PBNSIM_ENV_KERNEL_IMAGE=1: k_env builds its LDS image (no host-built image)
+    bool env_helpers = true;  // PBNSIM_ENV_HELPERS=0: no tail helpers (idle waves preparing a long session's blocks)
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
@@ -532,6 +533,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_LANES")) b->env_lane_limit = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_STEAL")) b->env_steal = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
+    if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -1061,12 +1063,18 @@ int pbn_mt_seed(pbn_batch* b, const uint64_t* seeds, int init_state) {
     HIP_TRY(hipMemcpyAsync(b->mt_seeds.p, seeds, 8 * b->B, hipMemcpyHostToDevice, b->stream));
     MTArgs a = mt_args(b);
     a.seeds = (const uint64_t*)b->mt_seeds.p;
-    a.init_state = init_state ? 1 : 0;
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
     int e = launch_mt_seed(b->W, a, b->grid_all(b->B), b->stream);
     if (e) return fail(PBN_E_HIP, "k_mt_seed launch: %s", hipGetErrorString((hipError_t)e));
     if (int rc = b->ev_end(stop)) return rc;
+    if (init_state) {  // genRandState / PBN.reset(None): the step kernel's init draws
+        a.init_state = 1;
+        if (int rc = b->ev_begin(&stop)) return rc;
+        e = launch_mt_step(b->W, a, b->n_cu, b->stream);
+        if (e) return fail(PBN_E_HIP, "k_mt_step (init) launch: %s", hipGetErrorString((hipError_t)e));
+        if (int rc = b->ev_end(stop)) return rc;
+    }
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->mt_ready = 1;
     return 0;
@@ -1081,7 +1089,7 @@ int pbn_mt_step(pbn_batch* b, uint32_t n_updates) {
     a.T = n_updates;
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
-    int e = launch_mt_step(b->W, a, b->grid_for(b->B, b->bpc_base), b->stream);
+    int e = launch_mt_step(b->W, a, b->n_cu, b->stream);
     if (e) return fail(PBN_E_HIP, "k_mt_step launch: %s", hipGetErrorString((hipError_t)e));
     return b->ev_end(stop);
 }
@@ -1535,9 +1543,10 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     b->steal_last = false;
     if (mode == 4 && b->env_steal && a.tail_max >= 1u && a.lane_limit >= 2u) {
         if (int rc = b->s_steal.ensure(8)) return rc;
-        HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, 4, b->stream));
+        HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, 8, b->stream));
         a.steal_local = 1;
-        a.steal_count = (uint32_t*)b->s_steal.p;
+        a.steal_count = (uint32_t*)b->s_steal.p;  // [0] envs handed off, [1] tail helpers recruited
+        a.tail_helpers = b->env_helpers ? 1 : 0;
         b->steal_last = true;
     }
     hipEvent_t stop;
@@ -1730,6 +1739,17 @@ int pbn_env_handoffs(pbn_batch* b, uint32_t* count) {
     if (!b->steal_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
     HIP_TRY(hipMemcpy(count, b->s_steal.p, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int pbn_env_tail_helpers(pbn_batch* b, uint32_t* count) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(count, "count");
+    SET_DEV(b);
+    *count = 0;
+    if (!b->steal_last) return 0;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipMemcpy(count, (const uint32_t*)b->s_steal.p + 1, 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -745,24 +745,40 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         return reinterpret_cast<uint32_t*>(lds + a.off_gen + w * GWB + CH * 128);
     };
     auto ldl = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    auto local_push = [&](uint64_t cand) {
-        if constexpr (TAIL) {
-            uint32_t claimed = 0;
-            if (lane == 0) {
-                uint32_t idle = ldl(&wctl[1]);
-                uint32_t n = min((uint32_t)__popc(idle), (uint32_t)__popcll(cand));
-                while (idle != 0u && n != 0u) {
-                    const uint32_t w = (uint32_t)__ffs(idle) - 1u, bit = 1u << w;
-                    idle &= ~bit;
-                    // acquire: the claimed wave cleared its flag before setting its idle bit (release), so
-                    // the flag / box writes below are ordered after that clear
-                    if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
-                        claimed |= bit;
-                        --n;
-                    }
+    // lane 0 claims up to n idle waves of the workgroup (clears their idle bits); wave-uniform result
+    auto claim_idle = [&](uint32_t n) -> uint32_t {
+        uint32_t claimed = 0;
+        if (lane == 0) {
+            uint32_t idle = ldl(&wctl[1]);
+            n = min((uint32_t)__popc(idle), n);
+            while (idle != 0u && n != 0u) {
+                const uint32_t w = (uint32_t)__ffs(idle) - 1u, bit = 1u << w;
+                idle &= ~bit;
+                // acquire: the claimed wave cleared its flag before setting its idle bit (release), so
+                // the flag / box writes that follow are ordered after that clear
+                if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
+                    claimed |= bit;
+                    --n;
                 }
             }
-            claimed = (uint32_t)__shfl((int)claimed, 0);
+        }
+        return (uint32_t)__shfl((int)claimed, 0);
+    };
+    // ---- tail helpers (TAIL, EnvArgs::tail_helpers): the ring a long tail session's blocks are prepared
+    // into, in the SESSION wave's draw buffer after its writer-mask table (the session wave, resolving
+    // only, does no writer rounds of its own): ring_R slots of one uint2 per lane per block, then the
+    // control words -- tags [8] (block index held by each slot), [8] cons (blocks below it are consumed),
+    // [9] stop, [10] helpers' acks, [12] u0, [13] c1, [14]/[15] gid, [16] first ring block, [17] helpers
+    const uint32_t wm_bytes = ((N + 31u) >> 5) * 256u;
+    const uint32_t ring_R = CH * 128u > wm_bytes + 80u ? min(8u, (CH * 128u - wm_bytes - 80u) / 512u) : 0u;
+    auto ring_of = [&](uint32_t w) { return lds + a.off_gen + w * GWB + wm_bytes; };
+    auto rctl_of = [&](uint32_t w) { return reinterpret_cast<uint32_t*>(ring_of(w) + ring_R * 512u); };
+    constexpr uint64_t HELP_MARK = 0xFFFFFFFFFFFFFFFEull;  // box[0] of a wave recruited as a helper
+    bool helping = false;
+    uint32_t help_req = 0;  // session wave | helper index << 8
+    auto local_push = [&](uint64_t cand) {
+        if constexpr (TAIL) {
+            const uint32_t claimed = claim_idle((uint32_t)__popcll(cand));
             if (claimed == 0u) return;
             const uint32_t k = (uint32_t)__popc(claimed);
             const uint32_t above = lane < 63u ? (uint32_t)__popcll(cand >> (lane + 1u)) : 0u;
@@ -799,7 +815,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
         }
     };
-    auto local_pop = [&]() -> bool {
+    auto local_pop = [&]() -> int {  // 0: leave, 1: an env in lane 0, 2: a helper request (help_req)
         if constexpr (TAIL) {
 #ifdef PBN_STAMPS
             const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
@@ -837,8 +853,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             est[17] += __builtin_amdgcn_s_memrealtime() - t_in;
             est[15] += got > 0 ? 1u : 0u;
 #endif
-            if (got < 0) return false;
+            if (got < 0) return 0;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (box_of(wv_in_wg)[0] == HELP_MARK) {  // recruited as a tail helper (every lane reads the box)
+                help_req = (uint32_t)box_of(wv_in_wg)[1];
+                if (lane == 0) __hip_atomic_store(flag_of(wv_in_wg), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return 2;
+            }
             if (lane == 0) {
                 const uint64_t* box = box_of(wv_in_wg);
                 e = (int64_t)box[0];
@@ -859,9 +880,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 capped = false;
                 __hip_atomic_store(flag_of(wv_in_wg), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            return true;
+            return 1;
         }
-        return false;
+        return 0;
     };
 
 
@@ -934,12 +955,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             }
         }
         const uint64_t act = __ballot(e >= 0);
-        if (act == 0) {
+        if (act == 0 && !helping) {
             if (__ballot(!exhausted) == 0) {
-                if (TAIL && a.steal_local && local_pop()) continue;  // a handed-off env in lane 0
-                break;
+                if (TAIL && a.steal_local) {
+                    const int r = local_pop();
+                    if (r == 1) continue;  // a handed-off env in lane 0
+                    if (r == 2) {
+                        helping = true;  // prepare another wave's tail blocks (the tail block below)
+                    } else {
+                        break;
+                    }
+                } else {
+                    break;
+                }
+            } else {
+                continue;
             }
-            continue;
         }
 #ifdef PBN_STAMPS
         if constexpr (GEN) {
@@ -977,11 +1008,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             // A long until-attractor loop left alone (the reference's unbounded loop,
             // pbn_target_multi.py:135-146, the per-step launch's last envs) then advances 64 updates
             // per block round trip instead of one per update.
-            if (tmode || (__popcll(act) <= a.tail_max && __ballot(exhausted) != 0)) {
+            if (tmode || helping || (__popcll(act) <= a.tail_max && __ballot(exhausted) != 0)) {
                 in_tail = true;
                 uint64_t* wm = reinterpret_cast<uint64_t*>(lds + a.off_gen + (threadIdx.x >> 6) * GWB);
                 if (!tmode) {
-                    for (uint32_t k = lane; k < N; k += 64) wm[k] = 0ull;
+                    for (uint32_t k = lane; k < wm_bytes / 8u; k += 64) wm[k] = 0ull;
                     wave_sync();
                     tmode = true;
                 }
@@ -990,20 +1021,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // config 5's 2^20 cap), so an env that has already run long is the likeliest to run longest;
                 // it goes first (the others are the ones handed to idle waves), so the wave's last env is
                 // not the long one queued behind the rest. Lowest lane when none has run past ENV_LONG_USED.
-                uint32_t L = (uint32_t)__ffsll((unsigned long long)act) - 1u;
-                if (__ballot(e >= 0 && used >= ENV_LONG_USED) != 0ull) {
-                    const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_max(e >= 0 ? used : 0u), 63);
-                    L = (uint32_t)__ffsll((unsigned long long)__ballot(e >= 0 && used == mx)) - 1u;
+                uint32_t L = act ? (uint32_t)__ffsll((unsigned long long)act) - 1u : 0u;  // (helping: unused)
+                if (!helping) {
+                    if (__ballot(e >= 0 && used >= ENV_LONG_USED) != 0ull) {
+                        const uint32_t mx =
+                            (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_max(e >= 0 ? used : 0u), 63);
+                        L = (uint32_t)__ffsll((unsigned long long)__ballot(e >= 0 && used == mx)) - 1u;
+                    }
+                    if (a.steal_local && (act & ~(1ull << L)) != 0ull) local_push(act & ~(1ull << L));
                 }
-                if (a.steal_local && (act & ~(1ull << L)) != 0ull) local_push(act & ~(1ull << L));
-                // the env's registers from lane L (wave-uniform index: v_readlane, no LDS permute)
+                // the env's registers from lane L (wave-uniform index: v_readlane, no LDS permute); a helper
+                // takes the session's update base, call index and env id from the session wave's ring control
                 auto from_L = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)L); };
-                uint32_t u = from_L(used);
+                const uint32_t* hrc = rctl_of(help_req & 0xFFu);
+                uint32_t u = helping ? hrc[12] : from_L(used);
                 uint32_t m = from_L(m_lo);
                 const uint32_t h0 = from_L(hit0 ? 1u : 0u);
-                const uint64_t gid = a.env_base + ((uint64_t)from_L((uint32_t)((uint64_t)e >> 32)) << 32 |
-                                                   (uint64_t)from_L((uint32_t)(uint64_t)e));
-                const uint32_t c1 = a.call_idx + from_L(t);
+                const uint64_t gid = helping ? ((uint64_t)hrc[15] << 32 | hrc[14])
+                                             : a.env_base + ((uint64_t)from_L((uint32_t)((uint64_t)e >> 32)) << 32 |
+                                                             (uint64_t)from_L((uint32_t)(uint64_t)e));
+                const uint32_t c1 = helping ? hrc[13] : a.call_idx + from_L(t);
                 uint32_t* col = P.base + ((int32_t)L - (int32_t)lane);  // lane L's plane column
                 const uint8_t* colb = reinterpret_cast<const uint8_t*>(col);
                 const uint4* erec = reinterpret_cast<const uint4*>(lds + a.L.off_rec);
@@ -1173,12 +1210,64 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     return A;
                 };
                 auto stageB = [&](const StA& A) { return erec[(A.ir + cnt4(A.t4, A.a32)) & 0xFFFFu]; };
+                if constexpr (ONE_ROW) {
+                    if (helping) {
+                        // ---- tail helper: blocks kb + j, kb + j + H, ... of the session wave's env, each
+                        // prepared exactly as the session would (draw, choice, env record, writer round in
+                        // this wave's own writer-mask table) and packed into the session's ring slot: the
+                        // record index | hm << 16 | min(nx, 64) << 20 (64: no later writer), rr. A slot is
+                        // written once the session has consumed the block R earlier (cons); the tag, stored
+                        // after the slot (release), tells the session which block the slot holds
+                        const uint32_t sw = help_req & 0xFFu, j = (help_req >> 8) & 0xFFu;
+                        uint8_t* const ring = ring_of(sw);
+                        uint32_t* const rcw = rctl_of(sw);
+                        const uint32_t kb = rcw[16], H = rcw[17];
+                        uint32_t slot = (kb + j) % ring_R;
+                        for (uint32_t b = kb + j;; b += H) {
+                            bool stop = false;
+                            for (;;) {
+                                if (ldl(&rcw[9]) != 0u) {
+                                    stop = true;
+                                    break;
+                                }
+                                if (b < ldl(&rcw[8]) + ring_R) break;
+                                __builtin_amdgcn_s_sleep(1);
+                            }
+                            if (stop) break;
+                            const StA Ah = stageA(b);
+                            const uint32_t idx = (Ah.ir + cnt4(Ah.t4, Ah.a32)) & 0xFFFFu;
+                            const uint4 qh = erec[idx];
+                            const TailDraw Dh = writers(qh, wround(qh));
+                            reinterpret_cast<uint2*>(ring + slot * 512u)[lane] =
+                                make_uint2(idx | (Dh.hm << 16) | (min(Dh.nx, 64u) << 20), Dh.rr);
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            if (lane == 0) __hip_atomic_store(&rcw[slot], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            slot += H;
+                            if (slot >= ring_R) slot -= ring_R;
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        if (lane == 0) (void)__hip_atomic_fetch_add(&rcw[10], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        helping = false;
+                        return;
+                    }
+                }
+                // ring mode (helpers recruited): the next block comes from the ring instead of stageA /
+                // stageB / the writer round; ringH = the session's helpers (0: self-prepared blocks)
+                uint32_t ringH = 0, rslot = 0;
+                uint32_t* const rcs = rctl_of(wv_in_wg);
+                const uint2* const rsl = reinterpret_cast<const uint2*>(ring_of(wv_in_wg));
                 TailDraw D = prepare(0u);
 #ifdef PBN_STAMPS
                 const uint64_t sess_rt = __builtin_amdgcn_s_memrealtime();
                 const uint32_t sess_u0 = u;
 #endif
-                for (uint32_t k = 0; !fin; ++k) {
+                uint32_t k = 0;
+                // the block loop, compiled twice: self-prepared blocks (RING false) until helpers are recruited,
+                // then blocks from the ring (RING true) -- separate instances, so neither path's live values
+                // weigh on the other's registers
+                auto blocks = [&](auto ring_c) {
+                constexpr bool RING = decltype(ring_c)::value;
+                for (; !fin; ++k) {
 #ifdef PBN_STAMPS
                     // tail block phases (shader clocks, s_memtime): 19 blocks, 20 cycles per block, 21 fixed-point
                     // rounds, 22 cycles of the resolution (fixed point), 23 cycles from the block's top to the
@@ -1198,10 +1287,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + (q.y >> 16));
                     [[maybe_unused]] StA An;
                     [[maybe_unused]] TailDraw Dn;
-                    if constexpr (SPLIT)
-                        An = stageA(k + 1u);  // while those reads are in flight
-                    else
+                    [[maybe_unused]] uint2 sd;
+                    if constexpr (SPLIT) {
+                        if constexpr (RING) {  // block k + 1 from the ring: wait for its tag, then its slot
+                            while (ldl(&rcs[rslot]) != k + 1u) __builtin_amdgcn_s_sleep(1);
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            sd = rsl[rslot * 64u + lane];
+                        } else {
+                            An = stageA(k + 1u);  // while those reads are in flight
+                        }
+                    } else {
                         Dn = prepare(k + 1u);
+                    }
 #ifdef PBN_STAMPS
                     const uint64_t c_prep = __builtin_amdgcn_s_memtime();
 #endif
@@ -1234,7 +1331,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                     y = yn;
                     [[maybe_unused]] uint4 qn;
-                    if constexpr (SPLIT) qn = stageB(An);
+                    if constexpr (SPLIT) {
+                        if constexpr (RING) {
+                            qn = erec[sd.x & 0xFFFFu];
+                            // block k + 1's slot is in registers: the slot is free (LDS keeps this wave's order;
+                            // the empty asm keeps the compiler from moving the store above the slot read)
+                            asm volatile("" ::"v"(sd.x), "v"(sd.y) : "memory");
+                            if (lane == 0) __hip_atomic_store(&rcs[8], k + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            rslot = rslot + 1u == ring_R ? 0u : rslot + 1u;
+                        } else {
+                            qn = stageB(An);
+                        }
+                    }
 #ifdef PBN_STAMPS
                     const uint64_t c_fp = __builtin_amdgcn_s_memtime();
 #endif
@@ -1253,10 +1361,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     u += nd;
                     hitf = SM != 0ull;
                     fin = hitf || u >= a.update_cap;
-                    if constexpr (SPLIT)
-                        D = writers(qn, wround(qn));
-                    else
+                    if constexpr (SPLIT) {
+                        if constexpr (RING) {
+                            D.q = qn;
+                            D.nd = *reinterpret_cast<const uint32_t*>(lds + (qn.w >> 16));
+                            D.hm = (sd.x >> 16) & 15u;
+                            D.nx = (sd.x >> 20) & 127u;  // 64: no later writer in the block (>= any prefix)
+                            D.rr = sd.y;
+                        } else {
+                            D = writers(qn, wround(qn));
+                        }
+                    } else {
                         D = Dn;  // (the commit above and the next block's plane reads stay in issue order)
+                    }
 #ifdef PBN_STAMPS
                     {
                         const uint64_t c_end = __builtin_amdgcn_s_memtime();
@@ -1271,11 +1388,62 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         est[24 + min(nround, 7u)] += 1;
                     }
 #endif
-                    // every 16 blocks: idle waves may have appeared since this env was started
-                    if (a.steal_local && (++nblk & 15u) == 0u) {
+                    // every 16 blocks: idle waves may have appeared since this env was started -- they take
+                    // this wave's unstarted envs first, then (a long session: >= 16 blocks) up to three of
+                    // the rest become its helpers, preparing blocks k + 2, k + 3, ... (D holds k + 1)
+                    if (a.steal_local && (++nblk & 15u) == 0u && !fin) {
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
                         if (others) local_push(others);
+                        if (SPLIT && !RING && a.tail_helpers && ring_R >= 4u && ldl(&wctl[1]) != 0u) {
+                            const uint32_t cl = claim_idle(3u);
+                            if (cl) {
+                                const uint32_t H = (uint32_t)__popc(cl), kb = k + 2u;
+                                if (lane < 8u) rcs[lane] = 0xFFFFFFFFu;  // tags: no block
+                                if (lane == 0) {
+                                    rcs[8] = kb;
+                                    rcs[9] = 0u;
+                                    rcs[10] = 0u;
+                                    rcs[12] = u0;
+                                    rcs[13] = c1;
+                                    rcs[14] = (uint32_t)gid;
+                                    rcs[15] = (uint32_t)(gid >> 32);
+                                    rcs[16] = kb;
+                                    rcs[17] = H;
+                                }
+                                uint32_t tw = 0;
+                                if (lane < H) {  // the lane-th claimed wave becomes helper `lane`
+                                    uint32_t c = cl;
+                                    for (uint32_t r = 0; r < lane; ++r) c &= c - 1u;
+                                    tw = (uint32_t)__ffs(c) - 1u;
+                                    box_of(tw)[0] = HELP_MARK;
+                                    box_of(tw)[1] = (uint64_t)(wv_in_wg | (lane << 8));
+                                }
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                                if (lane < H) {
+                                    (void)__hip_atomic_fetch_add(&wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    __hip_atomic_store(flag_of(tw), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                                if (lane == 0) atomicAdd(a.steal_count + 1, H);  // diagnostics (pbn_env_tail_helpers)
+                                ringH = H;
+                                rslot = kb % ring_R;
+                                ++k;
+                                return;  // on in the RING instance
+                            }
+                        }
                     }
+                }
+                };  // blocks
+                blocks(std::false_type{});
+                if (ringH) {
+                    blocks(std::true_type{});
+                    // release the helpers: stop, then wait until each has acknowledged (the ring lives in this
+                    // wave's draw buffer, which its next session reuses)
+                    if (lane == 0) {
+                        __hip_atomic_store(&rcs[9], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        while (ldl(&rcs[10]) != ringH) __builtin_amdgcn_s_sleep(1);
+                    }
+                    wave_sync();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
 #ifdef PBN_STAMPS
                 if ((u - sess_u0) / 64u > est[37]) {  // the wave's longest session: start, blocks, end, prior updates

@@ -14,12 +14,14 @@
 // by the lane itself when its position reaches 624 (sequential in-place MT19937).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pbn_device.hpp"
 #include "pbn_params.hpp"
 
 namespace pbn {
 
-constexpr uint32_t MT_N = 624, MT_M = 397;
+constexpr uint32_t MT_N = 624;  // (M = 397: the twist's offset, mt_twist_coop)
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
@@ -28,39 +30,6 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 18);
     return y;
 }
-
-__device__ void mt_twist(uint32_t* __restrict__ mt) {
-    uint32_t cur = mt[0];
-    for (uint32_t kk = 0; kk < MT_N; ++kk) {
-        const uint32_t nxt = mt[kk + 1 < MT_N ? kk + 1 : 0];  // mt[0] is already new when kk == 623
-        const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
-        const uint32_t src = mt[kk + MT_M < MT_N ? kk + MT_M : kk + MT_M - MT_N];
-        mt[kk] = src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-        cur = nxt;
-    }
-}
-
-struct MTStream {
-    uint32_t* row;
-    uint32_t pos;
-    __device__ __forceinline__ uint32_t next() {
-        if (pos >= MT_N) {
-            mt_twist(row);
-            pos = 0;
-        }
-        return mt_temper(row[pos++]);
-    }
-    // random.Random._randbelow_with_getrandbits(n), 1 <= n < 2^32 (CPython 3.10)
-    __device__ __forceinline__ uint32_t randbelow(uint32_t n, uint32_t kshift) {
-        uint32_t r = next() >> kshift;
-        while (r >= n) r = next() >> kshift;
-        return r;
-    }
-    __device__ __forceinline__ uint64_t k53() {
-        const uint32_t a = next(), b = next();
-        return k53_of(a, b);
-    }
-};
 
 __device__ void mt_init_genrand(uint32_t* mt, uint32_t s) {
     mt[0] = s;
@@ -106,92 +75,239 @@ __device__ void mt_seed_python(uint32_t* mt, uint64_t seed) {
 
 __device__ __forceinline__ uint32_t kshift_of(uint32_t n) { return (uint32_t)__clz(n); }  // 32 - bit_length(n)
 
-// Seed every env's generators; optionally run Graph.genRandState (base.py:368-370:
-// N x randint(0, 1)) or PBN.reset(None) (pbn.py:105-118: np.random.rand(N) > 0.5; state[0] = 0).
-template <int W, int KIND>
+// Seed every env's generators (random.seed(s): init_by_array; np.random.seed(s): init_genrand); the row
+// is left untwisted (pos 624: CPython's first draw twists). Graph.genRandState (base.py:368-370:
+// N x randint(0, 1)) / PBN.reset(None) (pbn.py:105-118: np.random.rand(N) > 0.5; state[0] = 0) then run as
+// k_mt_step with init_state = 1.
+template <int KIND>
 __global__ __launch_bounds__(BLOCK) void k_mt_seed(MTArgs a) {
     const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (e >= a.B) return;
     const uint64_t s = a.seeds[e];
-    uint32_t* py = a.mt_py + e * MT_ROW;
-    mt_seed_python(py, s);
+    mt_seed_python(a.mt_py + e * MT_ROW, s);
     a.pos_py[e] = MT_N;
-    uint32_t* np_row = nullptr;
     if constexpr (KIND == KIND_PROB_TABLE) {
-        np_row = a.mt_np + e * MT_ROW;
-        mt_init_genrand(np_row, (uint32_t)s);
+        mt_init_genrand(a.mt_np + e * MT_ROW, (uint32_t)s);
         a.pos_np[e] = MT_N;
     }
-    if (!a.init_state) return;
-    uint64_t st[W];
-#pragma unroll
-    for (int k = 0; k < W; ++k) st[k] = 0;
-    const uint32_t N = (uint32_t)a.n_nodes;
-    if constexpr (KIND == KIND_PREDICTOR_MIX) {
-        MTStream r{py, MT_N};
-        for (uint32_t i = 0; i < N; ++i) setbit<W>(st, i, r.randbelow(2u, kshift_of(2u)));
-        a.pos_py[e] = r.pos;
-    } else {
-        MTStream r{np_row, MT_N};
-        for (uint32_t i = 0; i < N; ++i) setbit<W>(st, i, r.k53() > (1ull << 52) ? 1u : 0u);
-        setbit<W>(st, 0u, 0u);
-        a.pos_np[e] = r.pos;
-    }
-    store_state<W>(a.state + e * W, st);
 }
 
 // T reference transitions per env from its own generators:
 //   Bittner Graph.step (base.py:306-312): i = randint(0, N-1); r = random() * CODsum
 //   PBN.step (pbn.py:129-133): i = randint(1, N-1) [stdlib]; u = np.random.uniform() [numpy]
+//
+// Each wave owns a tile of 64 envs (grid-stride over tiles). Per chunk of MT_CHUNK updates the wave first
+// GENERATES every lane's draws -- one MT word per lane per iteration through a small state machine
+// (node word with _randbelow's rejection, then the two words of random(); the truth-table network takes
+// its node from the `random` stream and its uniform from numpy's) -- into a per-lane LDS draw buffer,
+// then APPLIES them, every lane the same number of steps (no divergence on the rejection loop). A lane
+// reads its 2,496-B table row 16 B at a time (a window of the next 4 words, the following 4 prefetched).
+// The twist (every 624 words) is done by the whole wave for each row that needs it, 10 words per lane
+// in three phases (new[k] needs new[k - 227]: with k = 227 * phase + lane + 64 j that word is the same
+// lane's result of the previous phase), coalesced: lanes reach the end of their rows at different times
+// (rejection), and the in-lane twist this replaces serialised the wave on every one of them
+// (MT mode ran at ~1 % of its memory roofline).
+constexpr uint32_t MT_CHUNK = 8;  // draws per lane per generation pass (LDS: 8 B each; 8 keeps 4 workgroups per CU)
+constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu, MT_A = 0x9908b0dfu;
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
+    const uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
+    return m ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+}
+
+// Twist one row in place, all 64 lanes of the wave active (row: wave-uniform).
+__device__ __forceinline__ void mt_twist_coop(uint32_t* __restrict__ row, uint32_t lane) {
+    uint32_t o1[4], p1[4], m1[4], o2[4], p2[4], o3[3], p3[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t k1 = lane + 64u * j, k2 = 227u + lane + 64u * j;
+        const bool v1 = k1 < 227u;
+        o1[j] = v1 ? row[k1] : 0u;
+        p1[j] = v1 ? row[k1 + 1u] : 0u;
+        m1[j] = v1 ? row[k1 + 397u] : 0u;
+        o2[j] = v1 ? row[k2] : 0u;  // k2 < 454 exactly when k1 < 227
+        p2[j] = v1 ? row[k2 + 1u] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t k3 = 454u + lane + 64u * j;
+        o3[j] = k3 < 624u ? row[k3] : 0u;
+        p3[j] = k3 < 623u ? row[k3 + 1u] : 0u;
+    }
+    // every old word is read before any new word is written (other lanes read what this lane overwrites)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t n1[4], n2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        n1[j] = mt_mix(o1[j], p1[j], m1[j]);
+        n2[j] = mt_mix(o2[j], p2[j], n1[j]);
+    }
+    const uint32_t new0 = (uint32_t)__builtin_amdgcn_readlane((int)n1[0], 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t k1 = lane + 64u * j;
+        if (k1 < 227u) {
+            row[k1] = n1[j];
+            row[227u + k1] = n2[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t k3 = 454u + lane + 64u * j;
+        // k3 = 623 (lane 41, j = 2): mt[623] = mt[396] ^ f(mt[623], mt[0]) with mt[0], mt[396] already new
+        if (k3 < 624u) row[k3] = mt_mix(o3[j], k3 == 623u ? new0 : p3[j], n2[j]);
+    }
+}
+
+// One MT stream of one lane: row, next word index (624: twist first), 4-word window + prefetch
+struct MTWin {
+    uint32_t* row;
+    uint32_t pos;
+    uint4 cur, nxt;
+    __device__ __forceinline__ void load() {  // window at pos (pos < 624), prefetch of the next 4 words
+        const uint32_t g = pos & ~3u;
+        cur = *reinterpret_cast<const uint4*>(row + g);
+        if (g + 4u < MT_N) nxt = *reinterpret_cast<const uint4*>(row + g + 4u);
+    }
+    __device__ __forceinline__ uint32_t take() {  // the word at pos (tempered), pos + 1
+        const uint32_t q = pos & 3u;
+        const uint32_t w = q == 0u ? cur.x : q == 1u ? cur.y : q == 2u ? cur.z : cur.w;
+        ++pos;
+        if (q == 3u) {
+            cur = nxt;
+            if ((pos & ~3u) + 4u < MT_N) nxt = *reinterpret_cast<const uint4*>(row + (pos & ~3u) + 4u);
+        }
+        return mt_temper(w);
+    }
+};
+
 template <int W, int KIND>
 __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+    // per-lane draw buffer: [MT_CHUNK][BLOCK] u64 = k53 | node << 53
+    uint64_t* const dbuf = reinterpret_cast<uint64_t*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;
     const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint32_t lane = __lane_id();
+    constexpr bool TABLE = KIND == KIND_PROB_TABLE;
+    // node draw: randint(0, N-1) / randint(1, N-1) / the init bits (randint(0, 1) for Bittner)
+    const uint32_t nn = a.init_state ? 2u : (TABLE ? N - 1u : N);
+    const uint32_t ks = (uint32_t)__clz(nn);
     const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < a.B; e += stride) {
+    for (uint64_t e0 = (uint64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63u); e0 < a.B; e0 += stride) {
+        const uint64_t e = e0 + lane;
+        const bool valid = e < a.B;
+        const uint64_t ec = valid ? e : e0;  // lanes past B mirror lane 0's row (read only)
         uint64_t st[W];
-        load_state<W>(a.state + e * W, st);
-        to_plane<W>(P, st);
-        MTStream py{a.mt_py + e * MT_ROW, a.pos_py[e]};
-        if constexpr (KIND == KIND_PREDICTOR_MIX) {
-            const uint32_t ks = kshift_of(N);
-            for (uint32_t t = 0; t < a.T; ++t) {
-                const uint32_t i = py.randbelow(N, ks);
-                const uint64_t k53 = py.k53();
-                predictor_update_lds(P, i, k53, lds, a.L);
-            }
+        if (valid && !a.init_state) {
+            load_state<W>(a.state + e * W, st);
         } else {
-            MTStream np_{a.mt_np + e * MT_ROW, a.pos_np[e]};
-            const uint32_t ks = kshift_of(N - 1);
-            for (uint32_t t = 0; t < a.T; ++t) {
-                const uint32_t i = 1u + py.randbelow(N - 1, ks);
-                const uint64_t k53 = np_.k53();
-                table_update_lds(P, i, k53, lds, a.L);
-            }
-            a.pos_np[e] = np_.pos;
+#pragma unroll
+            for (int k = 0; k < W; ++k) st[k] = 0;
         }
-        a.pos_py[e] = py.pos;
-        from_plane<W>(P, st);
-        store_state<W>(a.state + e * W, st);
+        to_plane<W>(P, st);
+        MTWin py{a.mt_py + ec * MT_ROW, a.pos_py[ec], {}, {}};
+        MTWin np_{TABLE ? a.mt_np + ec * MT_ROW : nullptr, TABLE ? a.pos_np[ec] : 0u, {}, {}};
+        if (py.pos < MT_N) py.load();
+        if (TABLE && np_.pos < MT_N) np_.load();
+        // draws this launch: T updates, or N init draws (Bittner: N x randint(0, 1) from `random`;
+        // table: N x random_sample() from numpy, > 0.5)
+        uint32_t left = valid ? (a.init_state ? N : a.T) : 0u;
+        uint32_t done = 0;  // draws applied (init: the node index)
+        // machine: 0 node word (rejection), 1 first word of random(), 2 second word
+        uint32_t stt = (TABLE && a.init_state) ? 1u : 0u, node = 0, wa = 0;
+        while (__ballot(left > 0u) != 0ull) {
+            const uint32_t tgt = min(left, MT_CHUNK);
+            uint32_t cnt = 0;
+            for (;;) {
+                const bool want = cnt < tgt;
+                if (__ballot(want) == 0ull) break;
+                // the stream the next word comes from: `random` for the node word (and Bittner's random()),
+                // numpy for the table network's uniform
+                const bool from_np = TABLE && stt != 0u;
+                const bool tw_py = want && !from_np && py.pos >= MT_N;
+                const bool tw_np = TABLE && want && from_np && np_.pos >= MT_N;
+                uint64_t mask = __ballot(tw_py);
+                while (mask) {  // twist every row that has run out, one row per round, the whole wave
+                    const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                    mask &= mask - 1ull;
+                    const uint64_t eL = e0 + L;
+                    mt_twist_coop(a.mt_py + eL * MT_ROW, lane);
+                }
+                if constexpr (TABLE) {
+                    mask = __ballot(tw_np);
+                    while (mask) {
+                        const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                        mask &= mask - 1ull;
+                        mt_twist_coop(a.mt_np + (e0 + L) * MT_ROW, lane);
+                    }
+                }
+                if (__ballot(tw_py || tw_np) != 0ull) {
+                    // the twisted rows' new words (written by other lanes) are read next: stores done, L1 dropped
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    if (tw_py) {
+                        py.pos = 0;
+                        py.load();
+                    }
+                    if (tw_np) {
+                        np_.pos = 0;
+                        np_.load();
+                    }
+                }
+                if (want) {
+                    const uint32_t w = from_np ? np_.take() : py.take();
+                    if (stt == 0u) {
+                        const uint32_t r = w >> ks;  // _randbelow: getrandbits(bit_length(n)), rejected if >= n
+                        if (r < nn) {
+                            node = r;
+                            stt = a.init_state && !TABLE ? 3u : 1u;  // Bittner init: the draw is the bit itself
+                        }
+                    } else if (stt == 1u) {
+                        wa = w;
+                        stt = 2u;
+                    } else {
+                        const uint64_t k53 = k53_of(wa, w);
+                        dbuf[cnt * BLOCK] = k53 | ((uint64_t)node << 53);
+                        ++cnt;
+                        stt = (TABLE && a.init_state) ? 1u : 0u;
+                    }
+                    if (stt == 3u) {  // Bittner init bit
+                        dbuf[cnt * BLOCK] = (uint64_t)node << 53;
+                        ++cnt;
+                        stt = 0u;
+                    }
+                }
+            }
+            // apply the chunk: every lane its cnt draws (cnt == tgt: each lane finished its chunk)
+            for (uint32_t c = 0; c < tgt; ++c) {
+                const uint64_t d = dbuf[c * BLOCK];
+                const uint64_t k53 = d & ((1ull << 53) - 1ull);
+                const uint32_t r = (uint32_t)(d >> 53);
+                if (a.init_state) {
+                    const uint32_t i = done + c;
+                    const uint32_t bit = TABLE ? (k53 > (1ull << 52) ? 1u : 0u) : r;
+                    const uint32_t dw = i >> 5, sh = i & 31u;
+                    P.put(dw, (P.get(dw) & ~(1u << sh)) | (bit << sh));
+                } else if constexpr (KIND == KIND_PREDICTOR_MIX) {
+                    predictor_update_lds(P, r, k53, lds, a.L);
+                } else {
+                    table_update_lds(P, 1u + r, k53, lds, a.L);
+                }
+            }
+            done += tgt;
+            left -= tgt;
+        }
+        if (valid) {
+            if (TABLE && a.init_state) P.put(0, P.get(0) & ~1u);  // pbn.py reset: state[0] = 0
+            from_plane<W>(P, st);
+            store_state<W>(a.state + e * W, st);
+            a.pos_py[e] = py.pos;
+            if constexpr (TABLE) a.pos_np[e] = np_.pos;
+        }
     }
-}
-
-template <int KIND>
-static void* mt_seed_fn(int W) {
-    switch (W) {
-        case 1: return (void*)k_mt_seed<1, KIND>;
-        case 2: return (void*)k_mt_seed<2, KIND>;
-        case 3: return (void*)k_mt_seed<3, KIND>;
-        case 4: return (void*)k_mt_seed<4, KIND>;
-        case 5: return (void*)k_mt_seed<5, KIND>;
-        case 6: return (void*)k_mt_seed<6, KIND>;
-        case 7: return (void*)k_mt_seed<7, KIND>;
-        case 8: return (void*)k_mt_seed<8, KIND>;
-    }
-    return nullptr;
 }
 
 template <int KIND>
@@ -210,20 +326,28 @@ static void* mt_step_fn(int W) {
 }
 
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream) {
-    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? mt_seed_fn<KIND_PREDICTOR_MIX>(W) : mt_seed_fn<KIND_PROB_TABLE>(W);
-    if (!fn) return (int)hipErrorInvalidValue;
+    (void)W;
+    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? (void*)k_mt_seed<KIND_PREDICTOR_MIX> : (void*)k_mt_seed<KIND_PROB_TABLE>;
     MTArgs c = a;
     void* kargs[] = {&c};
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, 0, (hipStream_t)stream);
 }
 
-int launch_mt_step(int W, const MTArgs& a, int grid, void* stream) {
+uint32_t mt_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK + 8u * MT_CHUNK * BLOCK; }
+
+// grid: the resident workgroups (every wave walks 64-env tiles), capped by the tiles there are
+int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream) {
     void* fn = a.L.kind == KIND_PREDICTOR_MIX ? mt_step_fn<KIND_PREDICTOR_MIX>(W) : mt_step_fn<KIND_PROB_TABLE>(W);
     if (!fn) return (int)hipErrorInvalidValue;
+    const uint32_t lds = mt_lds_bytes(W, a.L.bytes);
+    int bpc = 0;
+    if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(fn), BLOCK, lds))
+        return (int)e;
+    const uint64_t want = (a.B + BLOCK - 1) / BLOCK;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)n_cu * (uint64_t)std::max(bpc, 1)));
     MTArgs c = a;
     void* kargs[] = {&c};
-    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, step_lds_bytes(W, a.L.bytes, BLOCK),
-                                (hipStream_t)stream);
+    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
 }
 
 }  // namespace pbn

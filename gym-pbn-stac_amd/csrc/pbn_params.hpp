@@ -121,6 +121,9 @@ struct EnvArgs {
     const void* gen_img;      // fast == 2 / 4: the LDS image as staged (host-built, pbn_abi.cpp env_gen_image);
                               // null: the kernel builds it from img
     uint32_t chunk;           // fast == 2 / 4: updates per lane between draw rounds (ENV_CHUNK_SMALL / _LARGE)
+    int32_t tail_helpers;     // fast == 4 (with steal_local): idle waves of the workgroup prepare a long tail
+                              // session's blocks ahead (draws, records, writer masks) into the session wave's
+                              // LDS ring, so the session wave only resolves (k_env, tail helpers)
 };
 
 constexpr uint32_t MT_ROW = 624;
@@ -140,11 +143,11 @@ struct MTArgs {
     uint64_t B;
     uint32_t T;             // transitions per launch (k_mt_step)
     int32_t n_nodes;
-    int32_t init_state;     // k_mt_seed: also run genRandState / PBN.reset(None)
+    int32_t init_state;     // k_mt_step: run genRandState / PBN.reset(None) (N init draws) instead of T updates
     const uint64_t* seeds;  // [B] (k_mt_seed)
     uint32_t* mt_py;        // [B][MT_ROW] CPython `random` state
     uint32_t* mt_np;        // [B][MT_ROW] numpy legacy RandomState (probability-table networks)
-    uint32_t* pos_py;       // [B] next word index (624 = twist before next use)
+    uint32_t* pos_py;       // [B] next word index (624 = twist before next use: k_mt_step twists it, coalesced)
     uint32_t* pos_np;
 };
 
@@ -227,7 +230,7 @@ int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* 
                    uint32_t chunk = ENV_CHUNK_LARGE);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes = 0, uint32_t chunk = ENV_CHUNK_LARGE);
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
-int launch_mt_step(int W, const MTArgs& a, int grid, void* stream);
+int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream);  // grid from the kernel's occupancy
 uint32_t ssd_block(const SSDArgs& a);
 uint32_t ssd_layout(int W, uint32_t image_bytes, int n_nodes, int n_targets, SSDArgs* a);
 int launch_ssd(int W, const SSDArgs& a, int grid, void* stream);

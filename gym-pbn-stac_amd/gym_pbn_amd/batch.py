@@ -405,6 +405,12 @@ class PBNBatch:
         L.check(L.lib.pbn_timing_read_each(self._h, buf, cap, C.byref(n)))
         return [buf[k] for k in range(min(n.value, cap))]
 
+    def env_tail_helpers(self) -> int:
+        """Tail helpers the last R6 launch recruited (idle waves preparing a long tail session's blocks)."""
+        n = C.c_uint32(0)
+        L.check(L.lib.pbn_env_tail_helpers(self._h, C.byref(n)))
+        return n.value
+
     def env_handoffs(self) -> int:
         """Envs the last R6 launch handed from tail-mode waves to idle ones (0 with the hand-off off)."""
         n = C.c_uint32(0)

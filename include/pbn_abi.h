@@ -255,6 +255,10 @@ int pbn_timing_read_each(pbn_batch *b, double *ms_each, uint64_t cap, uint64_t *
  * 0 when the hand-off was off). Syncs the batch stream. Diagnostics: the reference has no counterpart
  * (its until-attractor loop, pbn_target_multi.py:135-146, runs one env in one process). */
 int pbn_env_handoffs(pbn_batch *b, uint32_t *count);
+/* Tail helpers recruited during the last R6 env-step launch (env_kernel 4): idle waves of a workgroup that
+ * prepared a long tail session's blocks ahead of the session wave (draws, records, writer masks; the session
+ * wave only resolves). Syncs the batch stream. Diagnostics; PBNSIM_ENV_HELPERS=0 turns them off. */
+int pbn_env_tail_helpers(pbn_batch *b, uint32_t *count);
 
 #ifdef __cplusplus
 }

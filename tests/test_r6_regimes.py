@@ -306,7 +306,7 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     acts = _actions(np.random.default_rng(321), (T, B, A), net.n_nodes)
-    handed = []
+    handed, helpers = [], []
     if mode == "fused":
         dev = torch.device("cuda", 0)
         d_a = torch.from_numpy(acts).to(dev)
@@ -345,18 +345,26 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
     b.close()
 
 
+@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off"])
 @pytest.mark.parametrize("mode", ["per_step", "fused"])
-def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypatch, mode):
+def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypatch, mode, case):
     """A case in which the workgroup hand-off must happen: one workgroup (4 waves), two
     lanes per wave taking envs, 6 envs -- three waves hold two envs each, the fourth none and goes idle
     at once. Every env's first env step is long (its action row is chosen with the oracle so that
     each runs >= 2,048 updates: per env, action rows are tried on the oracle until one does), so a wave resolving its first env reaches its 16-block re-check
     (tail_session: every 16 blocks) with its second env unstarted while the idle wave waits: the
-    hand-off happens (asserted), and every output equals the oracle."""
+    hand-off happens (asserted), and every output equals the oracle.
+
+    ``helpers``: 2 envs, both taken by one wave (two lanes); at its 16-block re-check it hands its
+    unstarted env to an idle wave and recruits the other idle waves as tail helpers, which prepare its
+    blocks (draws, records, writer masks) into its LDS ring while it resolves them (asserted: helpers
+    recruited; exact against the oracle). ``helpers_off``: the same with PBNSIM_ENV_HELPERS=0 (none)."""
     import torch
 
     monkeypatch.setenv("PBNSIM_ENV_LANES", "2")
     monkeypatch.setenv("PBNSIM_ENV_GRID", "1")
+    if case == "helpers_off":
+        monkeypatch.setenv("PBNSIM_ENV_HELPERS", "0")
     import sys
     from pathlib import Path
 
@@ -370,7 +378,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
                 horizon=100)
     o = oracle_mod.Oracle(net)
-    B, seed, base, T, A, cap = 6, 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
+    B, seed, base, T, A, cap = (6 if case == "handoff" else 2), 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     # per env, the first candidate action row (oracle) whose first env step runs >= 2,048 updates
@@ -391,7 +399,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     assert np.array_equal(b.get_state(), st)
-    handed = []
+    handed, helpers = [], []
     if mode == "fused":
         dev = torch.device("cuda", 0)
         d_a = torch.from_numpy(acts).to(dev)
@@ -403,6 +411,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
                                    n_.data_ptr(), update_cap=cap)
         b.sync()
         handed.append(b.env_handoffs())
+        helpers.append(b.env_tail_helpers())
         got = [(o_[t].cpu().numpy().view(np.uint64), r_[t].cpu().numpy(), f_[t].cpu().numpy(),
                 n_[t].cpu().numpy().view(np.uint32)) for t in range(T)]
     else:
@@ -410,10 +419,15 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
         for t in range(T):
             got.append(b.env_step_multi(cfg, acts[t], update_cap=cap))
             handed.append(b.env_handoffs())
+            helpers.append(b.env_tail_helpers())
     info = b.info()
     assert info["env_kernel"] == 4 and info["env_lane_limit"] == 2 and info["env_grid"] == 1
     assert info["env_handoff"] == 1
     assert handed[0] > 0, handed  # the first launch (every env long) must hand off
+    if case == "helpers":
+        assert helpers[0] > 0, helpers  # ... and recruit the remaining idle waves as helpers
+    if case == "helpers_off":
+        assert sum(helpers) == 0, helpers
     for t in range(T):
         ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=cap)
         obs, rew, flags, nup = got[t]
