@@ -81,6 +81,7 @@ def parse():
     p.add_argument("--no-beyond-mall", dest="beyond_mall", action="store_false",
                    help="skip the 8M-env (state past the MALL) step-mode supplement that carries the HBM roofline")
     p.add_argument("--no-probe", dest="probe", action="store_false", help="skip the memory-floor probe")
+    p.add_argument("--no-mt", dest="mt", action="store_false", help="skip the MT-mode (reference RNG) supplement")
     p.add_argument("--dist-backend", default="nccl",
                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); gloo lets several "
                         "ranks share one GPU for rehearsals")
@@ -320,6 +321,41 @@ def config2_supplement(device):
             "step_env_steps_per_s": B / s, "step_us_per_launch": s * 1e6,
             "rollout_updates_per_launch": 256, "rollout_node_updates_per_s": B * 256 * 5 / (rms / 1e3),
             "rollout_lanes_per_env": lanes}
+
+
+MT_WORDS_PER_UPDATE = 256 / 199 + 2.0  # Bittner-199: randint(0, 198) takes 256/199 words on average, random() 2
+
+
+def mt_supplement(net, device, B=1 << 20, T=256, reps=3):
+    """MT mode: every env runs the reference's own CPython MT19937, seeded from the
+    Python seed alone (random.seed(s); genRandState(); Graph.step() x T, base.py:7,94,306-312,368-370) --
+    the path that reproduces the reference bit for bit from its seed. Bittner-199, 1,048,576 envs, T updates
+    per pbn_mt_step launch. Algorithmic bytes: the MT words an update consumes (MT_WORDS_PER_UPDATE) each
+    twisted once (read + written, 8 B per word: the 2,496-B table per 624 words) + the packed state read and
+    written once per launch; against the 8 TB/s HBM spec (the 2.5 GiB of tables are past the MALL)."""
+    import numpy as np
+
+    from gym_pbn_amd.batch import PBNBatch
+
+    b = PBNBatch(net, B, device=device, seed=1)
+    b.mt_seed(np.arange(B, dtype=np.uint64) + 12345, init_state=True)
+    b.mt_step(T)  # warm-up (also moves every env past its first twists)
+    b.sync()
+    b.timing(2)
+    for _ in range(reps):
+        b.mt_step(T)
+    b.timing(0)
+    ms, n = b.timing_read()
+    b.close()
+    s = ms / 1e3 / reps
+    alg = B * T * MT_WORDS_PER_UPDATE * 8 + 16 * net.n_words * B
+    return {"workload": f"MT mode (reference RNG streams on the device), Bittner-199, {B} envs, T = {T} updates "
+                        "per launch", "node_updates_per_s": B * T / s, "ms_per_launch": s * 1e3,
+            "roofline": {"bound": "hbm", "achieved": alg / s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / s / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+                         "alg_bytes_rule": f"{MT_WORDS_PER_UPDATE:.3f} MT words per update x 8 B (twist read + write) "
+                                           "+ 16W B of packed state per env per launch"},
+            "kernel": "pbn::k_mt_step (draw generation pass + cooperative twists, csrc/pbn_mt.hip)"}
 
 
 def rollout_supplement(net, B, device, seed, T, valu):
@@ -712,6 +748,8 @@ def main():
         sup["beyond_mall_8m"] = guarded(beyond_mall_supplement, net, device, args.seed, floor)
     if args.r6_chunks > 0:
         sup["config5_r6"] = guarded(r6_supplement, args, world, rank, device, dist, valu)
+    if args.mt and args.network == "bittner199":
+        sup["mt_mode"] = guarded(mt_supplement, net, device)
     copy = guarded(copy_bandwidth, device) if rank == 0 else None
 
     # ---- the headline: W warm-up launches, then exactly K timed launches
@@ -860,7 +898,7 @@ def main():
             "dist": {"backend": dist.get_backend() if dist is not None else None,
                      "world_size": dist.get_world_size() if dist is not None else 1, "per_rank": ranks},
             "shard_check": check,
-            "order": "supplements (rollout, config 2, 8M past-MALL, config 5) ran before the headline",
+            "order": "supplements (rollout, config 2, 8M past-MALL, config 5, MT mode) ran before the headline",
             **sup,
         }
         if world == 1 and not args.no_cpu_baseline:  # the host-core baseline: rank 0 at N = 1 only

@@ -174,7 +174,7 @@ struct pbn_batch {
     int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
     bool env_steal = true;    // PBNSIM_ENV_STEAL=0: no hand-off of tail envs between a workgroup's waves (k_env, mode 4)
     bool env_kernel_image = false;  // PBNSIM_ENV_KERNEL_IMAGE=1: k_env builds its LDS image (no host-built image)
-    bool env_helpers = true;  // PBNSIM_ENV_HELPERS=0: no tail helpers (idle waves preparing a long session's blocks)
+    int env_helpers = 3;      // PBNSIM_ENV_HELPERS: at most this many tail helpers per session (0-3; 0 = off)
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
@@ -533,7 +533,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_LANES")) b->env_lane_limit = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_STEAL")) b->env_steal = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
-    if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = atoi(v) != 0;
+    if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = std::max(0, std::min(3, atoi(v)));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -1542,11 +1542,13 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     // never holds two: off there
     b->steal_last = false;
     if (mode == 4 && b->env_steal && a.tail_max >= 1u && a.lane_limit >= 2u) {
-        if (int rc = b->s_steal.ensure(8)) return rc;
-        HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, 8, b->stream));
+        if (int rc = b->s_steal.ensure(16)) return rc;
+        HIP_TRY(hipMemsetAsync(b->s_steal.p, 0, 16, b->stream));
         a.steal_local = 1;
-        a.steal_count = (uint32_t*)b->s_steal.p;  // [0] envs handed off, [1] tail helpers recruited
-        a.tail_helpers = b->env_helpers ? 1 : 0;
+        // [0] envs handed off, [1] tail helpers recruited, [2] tail blocks read from helper rings, [3] of those,
+        // the ones whose helper had not written them when the session reached them
+        a.steal_count = (uint32_t*)b->s_steal.p;
+        a.tail_helpers = b->env_helpers;
         b->steal_last = true;
     }
     hipEvent_t stop;
@@ -1739,6 +1741,17 @@ int pbn_env_handoffs(pbn_batch* b, uint32_t* count) {
     if (!b->steal_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
     HIP_TRY(hipMemcpy(count, b->s_steal.p, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int pbn_env_tail_stats(pbn_batch* b, uint32_t* stats) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(stats, "stats");
+    SET_DEV(b);
+    for (int k = 0; k < 4; k++) stats[k] = 0;
+    if (!b->steal_last) return 0;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipMemcpy(stats, b->s_steal.p, 16, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -1254,6 +1254,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // ring mode (helpers recruited): the next block comes from the ring instead of stageA /
                 // stageB / the writer round; ringH = the session's helpers (0: self-prepared blocks)
                 uint32_t ringH = 0, rslot = 0;
+                uint2 sdN = make_uint2(0u, 0u);  // RING: the slot of the block after the current one
+                uint32_t rblocks = 0, rwaits = 0;  // RING diagnostics (pbn_env_tail_stats)
                 uint32_t* const rcs = rctl_of(wv_in_wg);
                 const uint2* const rsl = reinterpret_cast<const uint2*>(ring_of(wv_in_wg));
                 TailDraw D = prepare(0u);
@@ -1287,12 +1289,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + (q.y >> 16));
                     [[maybe_unused]] StA An;
                     [[maybe_unused]] TailDraw Dn;
-                    [[maybe_unused]] uint2 sd;
+                    [[maybe_unused]] uint2 sdNN;
+                    [[maybe_unused]] uint4 qn;
                     if constexpr (SPLIT) {
-                        if constexpr (RING) {  // block k + 1 from the ring: wait for its tag, then its slot
-                            while (ldl(&rcs[rslot]) != k + 1u) __builtin_amdgcn_s_sleep(1);
+                        if constexpr (RING) {
+                            // two blocks ahead: block k + 1's record (its slot, sdN, was read a block ago), and block
+                            // k + 2's slot once its tag says a helper has written it -- no LDS round trip of the
+                            // ring on the block's own chain (plane reads, fixed point, prefix, commit)
+                            qn = erec[sdN.x & 0xFFFFu];
+                            ++rblocks;
+                            if (ldl(&rcs[rslot]) != k + 2u) {
+                                ++rwaits;  // diagnostics: the block's helper had not written it yet
+                                while (ldl(&rcs[rslot]) != k + 2u) __builtin_amdgcn_s_sleep(1);
+                            }
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                            sd = rsl[rslot * 64u + lane];
+                            sdNN = rsl[rslot * 64u + lane];
                         } else {
                             An = stageA(k + 1u);  // while those reads are in flight
                         }
@@ -1330,14 +1341,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         yn = fround(y);
                     }
                     y = yn;
-                    [[maybe_unused]] uint4 qn;
                     if constexpr (SPLIT) {
                         if constexpr (RING) {
-                            qn = erec[sd.x & 0xFFFFu];
-                            // block k + 1's slot is in registers: the slot is free (LDS keeps this wave's order;
+                            // block k + 2's slot is in registers: its slot is free (LDS keeps this wave's order;
                             // the empty asm keeps the compiler from moving the store above the slot read)
-                            asm volatile("" ::"v"(sd.x), "v"(sd.y) : "memory");
-                            if (lane == 0) __hip_atomic_store(&rcs[8], k + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            asm volatile("" ::"v"(sdNN.x), "v"(sdNN.y) : "memory");
+                            if (lane == 0) __hip_atomic_store(&rcs[8], k + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             rslot = rslot + 1u == ring_R ? 0u : rslot + 1u;
                         } else {
                             qn = stageB(An);
@@ -1365,9 +1374,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         if constexpr (RING) {
                             D.q = qn;
                             D.nd = *reinterpret_cast<const uint32_t*>(lds + (qn.w >> 16));
-                            D.hm = (sd.x >> 16) & 15u;
-                            D.nx = (sd.x >> 20) & 127u;  // 64: no later writer in the block (>= any prefix)
-                            D.rr = sd.y;
+                            D.hm = (sdN.x >> 16) & 15u;
+                            D.nx = (sdN.x >> 20) & 127u;  // 64: no later writer in the block (>= any prefix)
+                            D.rr = sdN.y;
+                            sdN = sdNN;
                         } else {
                             D = writers(qn, wround(qn));
                         }
@@ -1395,7 +1405,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
                         if (others) local_push(others);
                         if (SPLIT && !RING && a.tail_helpers && ring_R >= 4u && ldl(&wctl[1]) != 0u) {
-                            const uint32_t cl = claim_idle(3u);
+                            const uint32_t cl = claim_idle(min((uint32_t)a.tail_helpers, 3u));
                             if (cl) {
                                 const uint32_t H = (uint32_t)__popc(cl), kb = k + 2u;
                                 if (lane < 8u) rcs[lane] = 0xFFFFFFFFu;  // tags: no block
@@ -1426,6 +1436,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                                 if (lane == 0) atomicAdd(a.steal_count + 1, H);  // diagnostics (pbn_env_tail_helpers)
                                 ringH = H;
                                 rslot = kb % ring_R;
+                                // block kb's slot before the RING instance starts (it reads two blocks ahead)
+                                while (ldl(&rcs[rslot]) != kb) __builtin_amdgcn_s_sleep(1);
+                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                                sdN = rsl[rslot * 64u + lane];
+                                asm volatile("" ::"v"(sdN.x), "v"(sdN.y) : "memory");
+                                if (lane == 0) __hip_atomic_store(&rcs[8], kb + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                rslot = rslot + 1u == ring_R ? 0u : rslot + 1u;
                                 ++k;
                                 return;  // on in the RING instance
                             }
@@ -1444,6 +1461,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     }
                     wave_sync();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (lane == 0) {
+                        atomicAdd(a.steal_count + 2, rblocks);
+                        atomicAdd(a.steal_count + 3, rwaits);
+                    }
                 }
 #ifdef PBN_STAMPS
                 if ((u - sess_u0) / 64u > est[37]) {  // the wave's longest session: start, blocks, end, prior updates

@@ -245,9 +245,12 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
                     }
                 }
                 if (__ballot(tw_py || tw_np) != 0ull) {
-                    // the twisted rows' new words (written by other lanes) are read next: stores done, L1 dropped
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    // the twisted rows' new words (written by other lanes of this wave) are read next: workgroup
+                    // scope (the wave's own CU, whose L1 the stores went through) -- an agent-scope fence here
+                    // wrote back and invalidated the L2 (buffer_wbl2 / buffer_inv sc1) at every twist
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (tw_py) {
                         py.pos = 0;
                         py.load();

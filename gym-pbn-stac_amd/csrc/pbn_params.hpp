@@ -121,7 +121,7 @@ struct EnvArgs {
     const void* gen_img;      // fast == 2 / 4: the LDS image as staged (host-built, pbn_abi.cpp env_gen_image);
                               // null: the kernel builds it from img
     uint32_t chunk;           // fast == 2 / 4: updates per lane between draw rounds (ENV_CHUNK_SMALL / _LARGE)
-    int32_t tail_helpers;     // fast == 4 (with steal_local): idle waves of the workgroup prepare a long tail
+    int32_t tail_helpers;     // fast == 4 (with steal_local): up to this many (<= 3) idle waves of the workgroup prepare a long tail
                               // session's blocks ahead (draws, records, writer masks) into the session wave's
                               // LDS ring, so the session wave only resolves (k_env, tail helpers)
 };

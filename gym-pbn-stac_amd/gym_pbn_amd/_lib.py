@@ -127,6 +127,7 @@ SIGNATURES = {
     "pbn_timing_read_each": (C.c_int, [_vp, C.POINTER(C.c_double), C.c_uint64, C.POINTER(C.c_uint64)]),
     "pbn_env_handoffs": (C.c_int, [_vp, _u32p]),
     "pbn_env_tail_helpers": (C.c_int, [_vp, _u32p]),
+    "pbn_env_tail_stats": (C.c_int, [_vp, _u32p]),
 }
 
 

@@ -411,6 +411,12 @@ class PBNBatch:
         L.check(L.lib.pbn_env_tail_helpers(self._h, C.byref(n)))
         return n.value
 
+    def env_tail_stats(self) -> dict:
+        """The last R6 launch's tail counters (hand-offs, helpers, ring blocks, ring blocks waited for)."""
+        st = (C.c_uint32 * 4)()
+        L.check(L.lib.pbn_env_tail_stats(self._h, st))
+        return {"handoffs": st[0], "helpers": st[1], "ring_blocks": st[2], "ring_waits": st[3]}
+
     def env_handoffs(self) -> int:
         """Envs the last R6 launch handed from tail-mode waves to idle ones (0 with the hand-off off)."""
         n = C.c_uint32(0)

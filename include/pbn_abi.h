@@ -259,6 +259,10 @@ int pbn_env_handoffs(pbn_batch *b, uint32_t *count);
  * prepared a long tail session's blocks ahead of the session wave (draws, records, writer masks; the session
  * wave only resolves). Syncs the batch stream. Diagnostics; PBNSIM_ENV_HELPERS=0 turns them off. */
 int pbn_env_tail_helpers(pbn_batch *b, uint32_t *count);
+/* The last R6 launch's tail counters, stats[4]: envs handed off, helpers recruited, tail blocks the
+ * sessions read from their helpers' rings, and of those the blocks not yet written when the session reached
+ * them (the session waited). Syncs the batch stream. Diagnostics. */
+int pbn_env_tail_stats(pbn_batch *b, uint32_t *stats);
 
 #ifdef __cplusplus
 }

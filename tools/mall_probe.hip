@@ -39,15 +39,21 @@ __global__ __launch_bounds__(1024) void k_probe(uint64_t* __restrict__ s, uint64
             // the envs whose updated bit changed
             // wbytes: 32 = the whole env (the kernel's store), 16 = the half holding the changed word,
             // 8 = only the changed word (word index from the env id, as the updated node's word varies)
-            auto wr = [&](ulonglong2* q, uint64_t e, ulonglong2 v0, ulonglong2 v1) {
-                const uint32_t wsel = (uint32_t)((e * 0x9E3779B97F4A7C15ull) >> 62);
-                if (wbytes >= 32u) {
+            auto wr = [&](ulonglong2* q, uint64_t e, const ulonglong2& v0, const ulonglong2& v1) {
+                if (wbytes >= 32u) {  // the kernel's store (the default, what bench.py's floor uses)
                     q[0] = v0;
                     q[1] = v1;
-                } else if (wbytes == 16u) {
-                    q[wsel >> 1] = (wsel >> 1) ? v1 : v0;
+                    return;
+                }
+                const uint32_t wsel = (uint32_t)(e * 0x9E3779B9u) >> 30;
+                if (wbytes == 16u) {
+                    if (wsel >> 1)
+                        q[1] = v1;
+                    else
+                        q[0] = v0;
                 } else {
-                    reinterpret_cast<uint64_t*>(q)[wsel] = v0.x ^ v1.y ^ wsel;
+                    uint64_t* w = reinterpret_cast<uint64_t*>(q) + wsel;
+                    *w = v0.x ^ v1.y;
                 }
             };
             if ((uint32_t)((((ea >> glog) ^ salt) * 2654435761u) >> 7) % 100u < write_pct) {

@@ -50,8 +50,12 @@ def main():
         "alg_bytes": 16 * ((json.loads((ROOT / "gym-pbn-stac_amd/gym_pbn_amd/data/networks.json").read_text())
                             ["networks"].get(network, {}).get("n_nodes", 199) + 63) // 64) * batch,
     }
+    import os
+    tree = os.environ.get("PMC_TREE", "unknown tree")  # the commit the caller profiled (no .git on the GPU box)
+    doc["detail"][f"{network}:{batch}"]["tree"] = tree
     doc["source"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on bench.py --kernel-only; "
-                     "per-launch median; FETCH_SIZE x2 (gfx950 wide-read correction), WRITE_SIZE as is")
+                     "per-launch median; FETCH_SIZE x2 (gfx950 wide-read correction), WRITE_SIZE as is; "
+                     f"profiled tree {tree}")
     out_path.write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps(doc["detail"][f"{network}:{batch}"]))
 

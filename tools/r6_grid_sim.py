@@ -9,6 +9,14 @@ and a 64-update tail block c_blk[ws] us, ws = the waves sharing the SIMD. Polici
   global counter (launch 2), P2 waves per SIMD, parked envs taken longest-first when ``order='used'``.
 * ``levels``: lane launches with refill from a compacted list of live envs, budgets K0, K1, ...; once
   the live count drops to <= tail_at envs, a tail launch as above.
+* ``global_handoff``: the ideal of an in-launch grid-wide hand-off (any idle wave takes any wave's unstarted
+  tail env at no cost) -- the bound on what moving envs between workgroups could give.
+
+Finding (profiles/r05_r6_grid_sim.txt): without knowing which envs will run long, the budget policy gains
+nothing (parked envs all have used = K, so "longest-used first" is a random order: 2.12 vs 2.15 ms at cap 2^20;
+with the exact remaining lengths as an oracle order, 1.55); even the ideal grid-wide hand-off gives 1.82 at the
+measured block cost (0.7 us) -- the lever is the tail block's cost: at 0.35 us the same schedules give
+1.1-1.7 ms. Hence round 5's tail helpers.
 
 Measurement tooling only (no product code reads it). Usage: python tools/r6_grid_sim.py nup_*.npy"""
 import heapq
@@ -85,6 +93,60 @@ def levels(nup, Ks, tail_at, ws=2, ws2=2, order='list'):
     return t + tail_phase(rem, SIMDS * ws2, ws2, order)
 
 
+def global_handoff(nup, c_blk=0.7, tail_max=16, lanes=64, c_chunk=48 * 0.25, c_draw=0.25, c_sess=2.0,
+                   c_push=1.0):
+    """The ideal of an in-launch GRID-wide hand-off (no cost to reach any idle wave): per wave lane mode until
+    <= tail_max live envs, then tail sessions, longest-used first; a wave's unstarted envs go to a grid-wide
+    pool (sorted by used) that ANY idle wave pulls from. Same constants as tools/r6_sched_sim.py."""
+    B = len(nup)
+    waves = []
+    for w in range(B // lanes):
+        E = [[int(x), 0] for x in nup[w * lanes:(w + 1) * lanes]]
+        t = 20.0
+        E = [e for e in E if e[0] > 0]
+        while len(E) > tail_max:
+            n = len(E)
+            t += c_chunk + c_draw * (math.ceil(n * 16 / 64) if n < 40 else 8) * 1.5
+            for e in E:
+                p = min(48, e[0])
+                e[0] -= p
+                e[1] += p
+            E = [e for e in E if e[0] > 0]
+        waves.append([t, E])
+    pool, cnt, idle, tend = [], 0, [], 0.0
+    ev = [(t, i) for i, (t, _) in enumerate(waves)]
+    heapq.heapify(ev)
+    while ev:
+        t, i = heapq.heappop(ev)
+        E = waves[i][1]
+        if not E:
+            if pool:
+                _, _, env = heapq.heappop(pool)
+                E = [env]
+                t += c_push
+            else:
+                idle.append((t, i))
+                tend = max(tend, t)
+                continue
+        k = max(range(len(E)), key=lambda j: E[j][1]) if any(e[1] >= 1024 for e in E) else 0
+        env, others = E[k], [e for j, e in enumerate(E) if j != k]
+        for e in others:
+            cnt += 1
+            heapq.heappush(pool, (-e[1], cnt, e))
+        while idle and pool:
+            ti, j = idle.pop()
+            _, _, e = heapq.heappop(pool)
+            waves[j][1] = [e]
+            heapq.heappush(ev, (max(ti, t) + c_push, j))
+        t += c_sess + math.ceil(env[0] / 64) * c_blk
+        env[1] += env[0]
+        env[0] = 0
+        waves[i][1] = []
+        heapq.heappush(ev, (t, i))
+        tend = max(tend, t)
+    return tend
+
+
 if __name__ == '__main__':
     D = {f.split('/')[-1]: np.load(f) for f in sys.argv[1:]}
 
@@ -98,3 +160,6 @@ if __name__ == '__main__':
     for Ks in ((128, 256, 512, 1024, 2048, 4096), (256, 1024, 4096), (512, 2048, 8192)):
         for ta in (2048, 4096, 8192):
             run(f'levels {Ks} tail<={ta}', lambda n, Ks=Ks, ta=ta: levels(n, Ks, ta))
+    for cb in (0.7, 0.35):
+        for tm in (16, 32):
+            run(f'ideal grid-wide hand-off c_blk {cb} tail {tm}', lambda n, cb=cb, tm=tm: global_handoff(n, cb, tm))

@@ -34,7 +34,12 @@ ROOT = Path(__file__).resolve().parents[1]
 SETS = {"valu": ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                  "GRBM_GUI_ACTIVE"],
         "lds": ["SQ_INSTS_LDS", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
-                "SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]}
+                "SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"],
+        # issue vs dependency-latency breakdown of the R6 kernels
+        "stall": ["SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                  "SQ_ACTIVE_INST_MISC", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"],
+        "insts": ["SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH", "SQ_WAVES",
+                  "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]}
 SET = sys.argv[1] if len(sys.argv) > 1 else "valu"
 COUNTERS = SETS[SET]
 
@@ -69,6 +74,25 @@ def main():
         ups = sum(u for _, u in items)
         tot = {c: sum(d.get(c, 0.0) for d, _ in items) for c in COUNTERS}
         wall = sum(d["t"] for d, _ in items)
+        if SET in ("stall", "insts"):
+            wc = max(tot["SQ_WAVE_CYCLES"], 1)
+            gui = tot["GRBM_GUI_ACTIVE"]
+            r = {"kernel": items[0][0]["name"], "launches": len(items), "node_updates": ups, "profiled_kernel_s": wall,
+                 # SQ_WAVE_CYCLES counts quad-cycles summed over waves (MI355X_MICROARCH.md): x 4 / (1,024 SIMDs x
+                 # the kernel's cycles, GRBM_GUI_ACTIVE / 8 XCDs) = mean resident waves per SIMD
+                 "resident_waves_per_simd": (4 * wc) / (1024 * gui / 8) if gui else None,
+                 "counters": tot, "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on "
+                                            "tools/valu_pmc_child.py"}
+            if SET == "stall":  # shares of wave time (all quad-cycle counters)
+                for c in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                          "SQ_ACTIVE_INST_MISC", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
+                    r[c.lower().replace("sq_", "") + "_frac"] = tot[c] / wc
+            else:  # instructions per node update
+                for c in ("SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH"):
+                    r[c.lower().replace("sq_insts_", "") + "_insts_per_update"] = tot[c] / ups
+                r["busy_frac"] = tot["SQ_BUSY_CYCLES"] / max(gui / 8, 1)
+            res[key] = r
+            continue
         if SET == "lds":
             res[key] = {"kernel": items[0][0]["name"], "launches": len(items), "node_updates": ups,
                         "lds_insts_per_update": tot["SQ_INSTS_LDS"] / ups,
@@ -88,7 +112,7 @@ def main():
                     "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
     doc = {"kernels": res, "valu_peak": "256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s "
                                         "(MI355X_MICROARCH.md: chip parameters, wave scheduling)"}
-    (ROOT / "gpurun_out" / f"r04_{SET}_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
+    (ROOT / "gpurun_out" / f"r05_{SET}_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps({k: {kk: v for kk, v in r.items() if kk not in ("counters", "source", "kernel")}
                       for k, r in res.items()}))
 
