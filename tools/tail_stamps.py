@@ -7,7 +7,9 @@ fixed-point resolution's cycles and rounds, and the blocks per round count.
 
 Workloads (argv[1]): "lone" = 64 envs, one per wave (the small-batch path: every wave in tail mode),
 fixture attractors, cap 4,096, one launch per env step -- the tail block alone on its SIMD;
-"highcap" = 131,072 envs per step at cap 2^20 (config 5's high_cap figure). Prints JSON.
+"highcap" = 131,072 envs per step at cap 2^20 (config 5's high_cap figure); "ring" = one env alone in one
+workgroup (two lanes per wave take envs, so the tail helpers of its idle waves prepare its blocks), cap 2^20,
+24 env steps (PBNSIM_ENV_HELPERS=0 for the same without helpers). Prints JSON.
 """
 import ctypes as C
 import json
@@ -29,7 +31,11 @@ def main():
     import torch
 
     mode = sys.argv[1] if len(sys.argv) > 1 else "lone"
-    B, CAP = {"lone": (64, 4096), "highcap": (131072, 1 << 20)}[mode]
+    B, CAP = {"lone": (64, 4096), "highcap": (131072, 1 << 20), "ring": (1, 1 << 20)}[mode]
+    if mode == "ring":  # one env, one workgroup, two lanes per wave: the tail helpers' ring (PBNSIM_ENV_HELPERS)
+        import os
+        os.environ.setdefault("PBNSIM_ENV_GRID", "1")
+        os.environ.setdefault("PBNSIM_ENV_LANES", "2")
     lib = _lib.lib
     lib.pbn_exp_env_stamps.argtypes = [C.c_void_p, C.c_size_t]
     z = np.load(ROOT / "tests" / "golden" / "r6_bittner199.npz", allow_pickle=False)
@@ -37,7 +43,7 @@ def main():
     cfg = EnvConfig(net, attractors_from_cubes(z["cube_care"], z["cube_value"], z["cube_attractor"], net.n_nodes),
                     horizon=100)
     dev = torch.device("cuda", 0)
-    A, W, T = 4, net.n_words, 8
+    A, W, T = 4, net.n_words, (24 if mode == "ring" else 8)
     g = torch.Generator(device=dev)
     g.manual_seed(0xAC7)
     v = torch.randint(1, net.n_nodes + 1, (T, B, A), device=dev, generator=g, dtype=torch.int32)
