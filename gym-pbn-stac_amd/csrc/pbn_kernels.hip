@@ -770,9 +770,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     // control words -- tags [8] (block index held by each slot), [8] cons (blocks below it are consumed),
     // [9] stop, [10] helpers' acks, [12] u0, [13] c1, [14]/[15] gid, [16] first ring block, [17] helpers
     const uint32_t wm_bytes = ((N + 31u) >> 5) * 256u;
-    const uint32_t ring_R = CH * 128u > wm_bytes + 80u ? min(8u, (CH * 128u - wm_bytes - 80u) / 512u) : 0u;
+    // ring blocks are 128 updates (two per lane: 16 B per lane, 1 KiB per slot). The ring may run over the
+    // session wave's own hand-off flag and box: those are unused while it is in a session (it clears its flag
+    // before it next goes idle). Helpers keep a 128-bit writer-mask table (2 x wm_bytes) below their own flag.
+    const uint32_t ring_R = (GWB > wm_bytes + 80u && 2u * wm_bytes <= CH * 128u)
+                                ? min(8u, (GWB - wm_bytes - 80u) / 1024u) : 0u;
     auto ring_of = [&](uint32_t w) { return lds + a.off_gen + w * GWB + wm_bytes; };
-    auto rctl_of = [&](uint32_t w) { return reinterpret_cast<uint32_t*>(ring_of(w) + ring_R * 512u); };
+    auto rctl_of = [&](uint32_t w) { return reinterpret_cast<uint32_t*>(ring_of(w) + ring_R * 1024u); };
     constexpr uint64_t HELP_MARK = 0xFFFFFFFFFFFFFFFEull;  // box[0] of a wave recruited as a helper
     bool helping = false;
     uint32_t help_req = 0;  // session wave | helper index << 8
@@ -1212,36 +1216,88 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 auto stageB = [&](const StA& A) { return erec[(A.ir + cnt4(A.t4, A.a32)) & 0xFFFFu]; };
                 if constexpr (ONE_ROW) {
                     if (helping) {
-                        // ---- tail helper: blocks kb + j, kb + j + H, ... of the session wave's env, each
-                        // prepared exactly as the session would (draw, choice, env record, writer round in
-                        // this wave's own writer-mask table) and packed into the session's ring slot: the
-                        // record index | hm << 16 | min(nx, 64) << 20 (64: no later writer), rr. A slot is
-                        // written once the session has consumed the block R earlier (cons); the tag, stored
-                        // after the slot (release), tells the session which block the slot holds
-                        const uint32_t sw = help_req & 0xFFu, j = (help_req >> 8) & 0xFFu;
+                        // ---- tail helper: ring blocks hj, hj + H, ... of the session wave's env. A ring block is
+                        // 128 updates, lane l taking updates 2l and 2l + 1 of it -- one Philox call (words 0-1
+                        // and 2-3) serves both. Each is prepared as the session would (predictor choice, env
+                        // record, and a writer round over 128-bit writer masks in this wave's own table: node
+                        // n's {even, odd} masks at 16 n) and packed into the session's ring slot, 16 B per lane:
+                        // the two record indices | hm bits and next-writer indices | the two updates' last-writer
+                        // codes (update t' = 2l' + h' as t', one byte per operand). A slot is written once the
+                        // session has consumed the block R earlier (cons); the tag, stored after the slot
+                        // (release), tells the session which block it holds
+                        const uint32_t sw = help_req & 0xFFu, hj = (help_req >> 8) & 0xFFu;
                         uint8_t* const ring = ring_of(sw);
                         uint32_t* const rcw = rctl_of(sw);
-                        const uint32_t kb = rcw[16], H = rcw[17];
-                        uint32_t slot = (kb + j) % ring_R;
-                        for (uint32_t b = kb + j;; b += H) {
+                        const uint32_t H = rcw[17];
+                        // zero the 128-bit table (its upper half may hold this wave's own old ring slots)
+                        for (uint32_t q2 = lane; q2 < wm_bytes / 8u; q2 += 64u)
+                            reinterpret_cast<uint4*>(wmc)[q2] = make_uint4(0u, 0u, 0u, 0u);
+                        wave_sync();
+                        auto nadr = [&](uint32_t off, uint32_t bit) {  // node entry {even, odd}
+                            return reinterpret_cast<unsigned long long*>(wmc + ((off >> 2) + (bit << 3)) * 2u);
+                        };
+                        const uint64_t bl = (1ull << lane) - 1ull, ul = (2ull << lane) - 1ull;
+                        // code of the last earlier writer (t' = 2 l' + h', 7 bits) and whether there is one
+                        auto lastw = [](const ulonglong2& M, uint64_t bE, uint64_t bO, uint32_t& any) -> uint32_t {
+                            const uint64_t E = M.x & bE, O = M.y & bO;
+                            const uint32_t te = E ? 2u * (63u - (uint32_t)__clzll((long long)E)) : 0u;
+                            const uint32_t to = O ? 2u * (63u - (uint32_t)__clzll((long long)O)) + 1u : 0u;
+                            any = (E | O) != 0ull ? 1u : 0u;
+                            return max(E ? te : 0u, O ? to : 0u);
+                        };
+                        auto nextw = [](const ulonglong2& M, uint64_t aE, uint64_t aO) -> uint32_t {  // 128: none
+                            const uint64_t E = M.x & aE, O = M.y & aO;
+                            const uint32_t te = E ? 2u * (uint32_t)(__ffsll((unsigned long long)E) - 1) : 128u;
+                            const uint32_t to = O ? 2u * (uint32_t)(__ffsll((unsigned long long)O) - 1) + 1u : 128u;
+                            return min(te, to);
+                        };
+                        const uint32_t cbase = u0 >> 1;  // the ring's first update is even
+                        uint32_t slot = hj % ring_R;
+                        for (uint32_t jb = hj;; jb += H) {
                             bool stop = false;
                             for (;;) {
                                 if (ldl(&rcw[9]) != 0u) {
                                     stop = true;
                                     break;
                                 }
-                                if (b < ldl(&rcw[8]) + ring_R) break;
+                                if (jb < ldl(&rcw[8]) + ring_R) break;
                                 __builtin_amdgcn_s_sleep(1);
                             }
                             if (stop) break;
-                            const StA Ah = stageA(b);
-                            const uint32_t idx = (Ah.ir + cnt4(Ah.t4, Ah.a32)) & 0xFFFFu;
-                            const uint4 qh = erec[idx];
-                            const TailDraw Dh = writers(qh, wround(qh));
-                            reinterpret_cast<uint2*>(ring + slot * 512u)[lane] =
-                                make_uint2(idx | (Dh.hm << 16) | (min(Dh.nx, 64u) << 20), Dh.rr);
+                            uint32_t w4[4];
+                            draw(cbase + 64u * jb + lane, w4);
+                            const uint32_t ie = philox_node<KIND>(w4[0], N), io = philox_node<KIND>(w4[2], N);
+                            uint32_t ire = __umul24(ie, X.rs), iro = __umul24(io, X.rs);
+                            asm volatile("" : "+v"(ire), "+v"(iro));
+                            const uint4 te4 = reinterpret_cast<const uint4*>(lds)[ie];
+                            const uint4 to4 = reinterpret_cast<const uint4*>(lds)[io];
+                            const uint32_t idxe = (ire + cnt4(te4, w4[1])) & 0xFFFFu, idxo = (iro + cnt4(to4, w4[3])) & 0xFFFFu;
+                            const uint4 qe = erec[idxe], qo = erec[idxo];
+                            unsigned long long* const owe = nadr(qe.y >> 16, qe.z >> 24);
+                            unsigned long long* const owo = nadr(qo.y >> 16, qo.z >> 24);
+                            atomicOr(owe, 1ull << lane);      // even update 2l: bit l of the node's even mask
+                            atomicOr(owo + 1, 1ull << lane);  // odd update 2l + 1: bit l of the odd mask
+                            auto rd = [&](unsigned long long* a2) { return *reinterpret_cast<const ulonglong2*>(a2); };
+                            const ulonglong2 me0 = rd(nadr(qe.x & 0xFFFFu, qe.z & 31u)), me1 = rd(nadr(qe.x >> 16, (qe.z >> 8) & 31u)),
+                                             me2 = rd(nadr(qe.y & 0xFFFFu, (qe.z >> 16) & 31u)), me3 = rd(owe);
+                            const ulonglong2 mo0 = rd(nadr(qo.x & 0xFFFFu, qo.z & 31u)), mo1 = rd(nadr(qo.x >> 16, (qo.z >> 8) & 31u)),
+                                             mo2 = rd(nadr(qo.y & 0xFFFFu, (qo.z >> 16) & 31u)), mo3 = rd(owo);
+                            *reinterpret_cast<ulonglong2*>(owe) = make_ulonglong2(0ull, 0ull);  // all zero after the round
+                            *reinterpret_cast<ulonglong2*>(owo) = make_ulonglong2(0ull, 0ull);
+                            // earlier than 2l: even l' < l, odd l' < l; earlier than 2l + 1: even l' <= l, odd l' < l
+                            uint32_t a0, a1, a2, a3, rre, rro, hme, hmo;
+                            rre = lastw(me0, bl, bl, a0) | (lastw(me1, bl, bl, a1) << 8) | (lastw(me2, bl, bl, a2) << 16) |
+                                  (lastw(me3, bl, bl, a3) << 24);
+                            hme = (a0 << 3) | (a1 << 2) | (a2 << 1) | a3;
+                            rro = lastw(mo0, ul, bl, a0) | (lastw(mo1, ul, bl, a1) << 8) | (lastw(mo2, ul, bl, a2) << 16) |
+                                  (lastw(mo3, ul, bl, a3) << 24);
+                            hmo = (a0 << 3) | (a1 << 2) | (a2 << 1) | a3;
+                            // later than 2l: even l' > l, odd l' >= l; later than 2l + 1: even and odd l' > l
+                            const uint32_t nxe = nextw(me3, ~ul, ~bl), nxo = nextw(mo3, ~ul, ~ul);
+                            reinterpret_cast<uint4*>(ring + slot * 1024u)[lane] =
+                                make_uint4(idxe | (idxo << 16), hme | (hmo << 4) | (nxe << 8) | (nxo << 16), rre, rro);
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            if (lane == 0) __hip_atomic_store(&rcw[slot], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (lane == 0) __hip_atomic_store(&rcw[slot], jb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             slot += H;
                             if (slot >= ring_R) slot -= ring_R;
                         }
@@ -1251,24 +1307,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         return;
                     }
                 }
-                // ring mode (helpers recruited): the next block comes from the ring instead of stageA /
-                // stageB / the writer round; ringH = the session's helpers (0: self-prepared blocks)
-                uint32_t ringH = 0, rslot = 0;
-                uint2 sdN = make_uint2(0u, 0u);  // RING: the slot of the block after the current one
-                uint32_t rblocks = 0, rwaits = 0;  // RING diagnostics (pbn_env_tail_stats)
+                // ring mode (helpers recruited): ringH = the session's helpers (0: self-prepared blocks)
+                uint32_t ringH = 0;
+                uint32_t rblocks = 0, rwaits = 0;  // ring diagnostics (pbn_env_tail_stats)
                 uint32_t* const rcs = rctl_of(wv_in_wg);
-                const uint2* const rsl = reinterpret_cast<const uint2*>(ring_of(wv_in_wg));
                 TailDraw D = prepare(0u);
 #ifdef PBN_STAMPS
                 const uint64_t sess_rt = __builtin_amdgcn_s_memrealtime();
                 const uint32_t sess_u0 = u;
 #endif
                 uint32_t k = 0;
-                // the block loop, compiled twice: self-prepared blocks (RING false) until helpers are recruited,
-                // then blocks from the ring (RING true) -- separate instances, so neither path's live values
-                // weigh on the other's registers
-                auto blocks = [&](auto ring_c) {
-                constexpr bool RING = decltype(ring_c)::value;
+                // the self-prepared block loop; when helpers are recruited it returns and ring128 below resolves
+                // the rest of the session from their ring (separate code, its own registers)
+                auto blocks = [&]() {
                 for (; !fin; ++k) {
 #ifdef PBN_STAMPS
                     // tail block phases (shader clocks, s_memtime): 19 blocks, 20 cycles per block, 21 fixed-point
@@ -1289,27 +1340,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     const uint32_t b3 = *reinterpret_cast<const uint32_t*>(colb + (q.y >> 16));
                     [[maybe_unused]] StA An;
                     [[maybe_unused]] TailDraw Dn;
-                    [[maybe_unused]] uint2 sdNN;
                     [[maybe_unused]] uint4 qn;
-                    if constexpr (SPLIT) {
-                        if constexpr (RING) {
-                            // two blocks ahead: block k + 1's record (its slot, sdN, was read a block ago), and block
-                            // k + 2's slot once its tag says a helper has written it -- no LDS round trip of the
-                            // ring on the block's own chain (plane reads, fixed point, prefix, commit)
-                            qn = erec[sdN.x & 0xFFFFu];
-                            ++rblocks;
-                            if (ldl(&rcs[rslot]) != k + 2u) {
-                                ++rwaits;  // diagnostics: the block's helper had not written it yet
-                                while (ldl(&rcs[rslot]) != k + 2u) __builtin_amdgcn_s_sleep(1);
-                            }
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                            sdNN = rsl[rslot * 64u + lane];
-                        } else {
-                            An = stageA(k + 1u);  // while those reads are in flight
-                        }
-                    } else {
+                    if constexpr (SPLIT)
+                        An = stageA(k + 1u);  // while those reads are in flight
+                    else
                         Dn = prepare(k + 1u);
-                    }
 #ifdef PBN_STAMPS
                     const uint64_t c_prep = __builtin_amdgcn_s_memtime();
 #endif
@@ -1341,17 +1376,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         yn = fround(y);
                     }
                     y = yn;
-                    if constexpr (SPLIT) {
-                        if constexpr (RING) {
-                            // block k + 2's slot is in registers: its slot is free (LDS keeps this wave's order;
-                            // the empty asm keeps the compiler from moving the store above the slot read)
-                            asm volatile("" ::"v"(sdNN.x), "v"(sdNN.y) : "memory");
-                            if (lane == 0) __hip_atomic_store(&rcs[8], k + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            rslot = rslot + 1u == ring_R ? 0u : rslot + 1u;
-                        } else {
-                            qn = stageB(An);
-                        }
-                    }
+                    if constexpr (SPLIT) qn = stageB(An);
 #ifdef PBN_STAMPS
                     const uint64_t c_fp = __builtin_amdgcn_s_memtime();
 #endif
@@ -1370,20 +1395,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     u += nd;
                     hitf = SM != 0ull;
                     fin = hitf || u >= a.update_cap;
-                    if constexpr (SPLIT) {
-                        if constexpr (RING) {
-                            D.q = qn;
-                            D.nd = *reinterpret_cast<const uint32_t*>(lds + (qn.w >> 16));
-                            D.hm = (sdN.x >> 16) & 15u;
-                            D.nx = (sdN.x >> 20) & 127u;  // 64: no later writer in the block (>= any prefix)
-                            D.rr = sdN.y;
-                            sdN = sdNN;
-                        } else {
-                            D = writers(qn, wround(qn));
-                        }
-                    } else {
+                    if constexpr (SPLIT)
+                        D = writers(qn, wround(qn));
+                    else
                         D = Dn;  // (the commit above and the next block's plane reads stay in issue order)
-                    }
 #ifdef PBN_STAMPS
                     {
                         const uint64_t c_end = __builtin_amdgcn_s_memtime();
@@ -1400,24 +1415,24 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
                     // every 16 blocks: idle waves may have appeared since this env was started -- they take
                     // this wave's unstarted envs first, then (a long session: >= 16 blocks) up to three of
-                    // the rest become its helpers, preparing blocks k + 2, k + 3, ... (D holds k + 1)
+                    // the rest become its helpers, preparing the session's updates from u on in 128-update
+                    // ring blocks (the self-prepared block k + 1 in D is dropped)
                     if (a.steal_local && (++nblk & 15u) == 0u && !fin) {
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
                         if (others) local_push(others);
-                        if (SPLIT && !RING && a.tail_helpers && ring_R >= 4u && ldl(&wctl[1]) != 0u) {
+                        if (SPLIT && a.tail_helpers && ring_R >= 3u && ldl(&wctl[1]) != 0u) {
                             const uint32_t cl = claim_idle(min((uint32_t)a.tail_helpers, 3u));
                             if (cl) {
-                                const uint32_t H = (uint32_t)__popc(cl), kb = k + 2u;
+                                const uint32_t H = (uint32_t)__popc(cl);
                                 if (lane < 8u) rcs[lane] = 0xFFFFFFFFu;  // tags: no block
                                 if (lane == 0) {
-                                    rcs[8] = kb;
-                                    rcs[9] = 0u;
-                                    rcs[10] = 0u;
-                                    rcs[12] = u0;
+                                    rcs[8] = 0u;   // cons: ring blocks consumed
+                                    rcs[9] = 0u;   // stop
+                                    rcs[10] = 0u;  // acks
+                                    rcs[12] = u;   // the ring's first update (even: a block boundary)
                                     rcs[13] = c1;
                                     rcs[14] = (uint32_t)gid;
                                     rcs[15] = (uint32_t)(gid >> 32);
-                                    rcs[16] = kb;
                                     rcs[17] = H;
                                 }
                                 uint32_t tw = 0;
@@ -1435,24 +1450,163 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                                 }
                                 if (lane == 0) atomicAdd(a.steal_count + 1, H);  // diagnostics (pbn_env_tail_helpers)
                                 ringH = H;
-                                rslot = kb % ring_R;
-                                // block kb's slot before the RING instance starts (it reads two blocks ahead)
-                                while (ldl(&rcs[rslot]) != kb) __builtin_amdgcn_s_sleep(1);
-                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                                sdN = rsl[rslot * 64u + lane];
-                                asm volatile("" ::"v"(sdN.x), "v"(sdN.y) : "memory");
-                                if (lane == 0) __hip_atomic_store(&rcs[8], kb + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                rslot = rslot + 1u == ring_R ? 0u : rslot + 1u;
-                                ++k;
-                                return;  // on in the RING instance
+                                return;  // on in ring128
                             }
                         }
                     }
                 }
                 };  // blocks
-                blocks(std::false_type{});
+                // ---- the rest of the session from the helpers' ring, 128 updates per block: lane l resolves updates
+                // t = 2l and 2l + 1 (u + t). Per block: the 8 operand reads from the plane, a fixed point over both
+                // halves (round: one ballot per half; an operand written earlier in the block reads bit t' >> 1 of
+                // the ballot of t''s half), the counter prefix in update order (per lane the pair's sum, one wave
+                // prefix), the first update that hits a cube, and the last writers' commits. The ring is read two
+                // blocks ahead: block j + 1's records are issued and block j + 2's slot polled while j resolves.
+                auto ring128 = [&]() {
+                    const uint4* const rs4 = reinterpret_cast<const uint4*>(ring_of(wv_in_wg));
+                    auto poll = [&](uint32_t jb, uint32_t sl) {
+                        if (ldl(&rcs[sl]) != jb) {
+                            ++rwaits;  // diagnostics: the block's helper had not written it yet
+                            while (ldl(&rcs[sl]) != jb) __builtin_amdgcn_s_sleep(1);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        return rs4[sl * 64u + lane];
+                    };
+                    auto nxt_slot = [&](uint32_t sl) { return sl + 1u == ring_R ? 0u : sl + 1u; };
+                    auto nd_of = [&](const uint4& qq) { return *reinterpret_cast<const uint32_t*>(lds + (qq.w >> 16)); };
+                    uint4 sC = poll(0u, 0u);
+                    uint4 sN = poll(1u, nxt_slot(0u));
+                    asm volatile("" ::"v"(sN.x), "v"(sN.w) : "memory");
+                    if (lane == 0) __hip_atomic_store(&rcs[8], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    uint32_t rsl = nxt_slot(nxt_slot(0u));  // slot of block j + 2
+                    uint4 qe = erec[sC.x & 0xFFFFu], qo = erec[sC.x >> 16];
+                    uint32_t nde = nd_of(qe), ndo = nd_of(qo), inf = sC.y, rre = sC.z, rro = sC.w;
+                    auto look = [](uint64_t Ye, uint64_t Yo, uint32_t c) {  // output of update c (= 2 l' + h')
+                        return (uint32_t)(((c & 1u) ? Yo : Ye) >> (c >> 1)) & 1u;
+                    };
+                    for (uint32_t jb = 0; !fin; ++jb) {
+                        ++rblocks;
+#ifdef PBN_STAMPS
+                        // the same tail-block stamps as the self-prepared loop (est 19-31; rounds count fround calls)
+                        const uint64_t c_top = __builtin_amdgcn_s_memtime();
+                        const uint64_t r_top = __builtin_amdgcn_s_memrealtime();
+                        if (!est[34]) est[34] = r_top;
+                        uint32_t nround = 0;
+#endif
+                        const uint32_t se = qe.z >> 24, so = qo.z >> 24;
+                        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(colb + (qe.x & 0xFFFFu));
+                        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(colb + (qe.x >> 16));
+                        const uint32_t e2 = *reinterpret_cast<const uint32_t*>(colb + (qe.y & 0xFFFFu));
+                        const uint32_t e3 = *reinterpret_cast<const uint32_t*>(colb + (qe.y >> 16));
+                        const uint32_t o0 = *reinterpret_cast<const uint32_t*>(colb + (qo.x & 0xFFFFu));
+                        const uint32_t o1 = *reinterpret_cast<const uint32_t*>(colb + (qo.x >> 16));
+                        const uint32_t o2 = *reinterpret_cast<const uint32_t*>(colb + (qo.y & 0xFFFFu));
+                        const uint32_t o3 = *reinterpret_cast<const uint32_t*>(colb + (qo.y >> 16));
+                        // block j + 1's records, block j + 2's slot (in flight while this block resolves)
+                        const uint4 qe2 = erec[sN.x & 0xFFFFu], qo2 = erec[sN.x >> 16];
+                        const uint4 sNN = poll(jb + 2u, rsl);
+#ifdef PBN_STAMPS
+                        const uint64_t c_prep = __builtin_amdgcn_s_memtime();
+#endif
+                        const uint32_t v3e = __builtin_amdgcn_ubfe(e3, se, 1), v3o = __builtin_amdgcn_ubfe(o3, so, 1);
+                        const uint32_t p0e = (__builtin_amdgcn_ubfe(e0, qe.z, 1) << 3) | (__builtin_amdgcn_ubfe(e1, qe.z >> 8, 1) << 2) |
+                                             (__builtin_amdgcn_ubfe(e2, qe.z >> 16, 1) << 1) | v3e;
+                        const uint32_t p0o = (__builtin_amdgcn_ubfe(o0, qo.z, 1) << 3) | (__builtin_amdgcn_ubfe(o1, qo.z >> 8, 1) << 2) |
+                                             (__builtin_amdgcn_ubfe(o2, qo.z >> 16, 1) << 1) | v3o;
+                        const uint32_t hme = inf & 15u, hmo = (inf >> 4) & 15u, nxe = (inf >> 8) & 255u, nxo = (inf >> 16) & 255u;
+                        const uint32_t pfe = p0e & ~hme, pfo = p0o & ~hmo;
+                        uint32_t xe, xo;
+                        auto fround = [&](uint32_t ye_, uint32_t yo_, uint32_t& yne, uint32_t& yno) {
+#ifdef PBN_STAMPS
+                            ++nround;
+#endif
+                            const uint64_t Ye = __ballot(ye_ != 0u), Yo = __ballot(yo_ != 0u);
+                            const uint32_t pe = pfe | ((look(Ye, Yo, rre & 255u) & (hme >> 3)) << 3) |
+                                                ((look(Ye, Yo, (rre >> 8) & 255u) & (hme >> 2) & 1u) << 2) |
+                                                ((look(Ye, Yo, (rre >> 16) & 255u) & (hme >> 1) & 1u) << 1) |
+                                                (look(Ye, Yo, rre >> 24) & hme & 1u);
+                            const uint32_t po = pfo | ((look(Ye, Yo, rro & 255u) & (hmo >> 3)) << 3) |
+                                                ((look(Ye, Yo, (rro >> 8) & 255u) & (hmo >> 2) & 1u) << 2) |
+                                                ((look(Ye, Yo, (rro >> 16) & 255u) & (hmo >> 1) & 1u) << 1) |
+                                                (look(Ye, Yo, rro >> 24) & hmo & 1u);
+                            xe = pe & 1u;
+                            xo = po & 1u;
+                            yne = __builtin_amdgcn_ubfe(qe.w, pe, 1);
+                            yno = __builtin_amdgcn_ubfe(qo.w, po, 1);
+                        };
+                        uint32_t ye = __builtin_amdgcn_ubfe(qe.w, p0e, 1), yo = __builtin_amdgcn_ubfe(qo.w, p0o, 1);
+                        uint32_t yne, yno;
+                        fround(ye, yo, yne, yno);
+                        while (__ballot(yne != ye || yno != yo) != 0ull) {
+                            ye = yne;
+                            yo = yno;
+                            fround(ye, yo, yne, yno);
+                        }
+                        ye = yne;
+                        yo = yno;
+#ifdef PBN_STAMPS
+                        const uint64_t c_fp = __builtin_amdgcn_s_memtime();
+#endif
+                        // block j + 2's slot is in registers: it is free (the asm keeps the store after the read)
+                        asm volatile("" ::"v"(sNN.x), "v"(sNN.w) : "memory");
+                        if (lane == 0) __hip_atomic_store(&rcs[8], jb + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        rsl = nxt_slot(rsl);
+                        // packed counter deltas in update order: the pair's sum prefixed over the lanes
+                        const uint32_t sge = ye - 1u, sgo = yo - 1u;
+                        const uint32_t de = ((nde & (0u - (ye ^ xe))) ^ sge) - sge;
+                        const uint32_t dodd = ((ndo & (0u - (yo ^ xo))) ^ sgo) - sgo;
+                        const uint32_t pro = m + wave_inclusive_add(de + dodd), pre = pro - dodd;
+                        const uint32_t nvalid = a.update_cap > u ? min(128u, a.update_cap - u) : 0u;
+                        const bool ve = 2u * lane < nvalid, vo = 2u * lane + 1u < nvalid;
+                        // (no first-update test here: a ring starts 16 blocks into a session, u > 0)
+                        const uint64_t SMe = __ballot(ve && has_zero_byte(pre) != 0u);
+                        const uint64_t SMo = __ballot(vo && has_zero_byte(pro) != 0u);
+                        const uint32_t te = SMe ? 2u * (uint32_t)(__ffsll((unsigned long long)SMe) - 1) : 256u;
+                        const uint32_t to = SMo ? 2u * (uint32_t)(__ffsll((unsigned long long)SMo) - 1) + 1u : 256u;
+                        const uint32_t ts = min(te, to);
+                        const uint32_t nd = ts < 256u ? ts + 1u : nvalid;
+                        // commit: the last writer of each node among the first nd updates (both halves of a lane may
+                        // write; nx says whether a later update of the prefix writes the same node)
+                        if (2u * lane < nd && nxe >= nd && ye != v3e)
+                            atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + (qe.y >> 16)), 1u << se);
+                        if (2u * lane + 1u < nd && nxo >= nd && yo != v3o)
+                            atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + (qo.y >> 16)), 1u << so);
+                        m = (uint32_t)__builtin_amdgcn_readlane((int)(((nd - 1u) & 1u) ? pro : pre), (int)((nd - 1u) >> 1));
+                        u += nd;
+                        hitf = ts < 256u;
+                        fin = hitf || u >= a.update_cap;
+                        qe = qe2;
+                        qo = qo2;
+                        nde = nd_of(qe);
+                        ndo = nd_of(qo);
+                        inf = sN.y;
+                        rre = sN.z;
+                        rro = sN.w;
+                        sN = sNN;
+#ifdef PBN_STAMPS
+                        {
+                            const uint64_t c_end = __builtin_amdgcn_s_memtime();
+                            const uint64_t r_end = __builtin_amdgcn_s_memrealtime();
+                            est[32] += r_end - r_top;
+                            est[35] = r_end;
+                            est[19] += 1;
+                            est[20] += c_end - c_top;
+                            est[21] += nround;
+                            est[22] += c_fp - c_prep;
+                            est[23] += c_prep - c_top;
+                            est[24 + min(nround, 7u)] += 1;
+                        }
+#endif
+                        // every 8 ring blocks (1,024 updates): idle waves may take this wave's unstarted envs
+                        if ((jb & 7u) == 7u && !fin) {
+                            const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
+                            if (others) local_push(others);
+                        }
+                    }
+                };
+                blocks();
                 if (ringH) {
-                    blocks(std::true_type{});
+                    ring128();
                     // release the helpers: stop, then wait until each has acknowledged (the ring lives in this
                     // wave's draw buffer, which its next session reuses)
                     if (lane == 0) {
