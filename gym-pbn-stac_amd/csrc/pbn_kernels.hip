@@ -583,6 +583,9 @@ __device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) { return (v - 0x01
 #define PBN_ENV_OWN_DRAWS_MIN 40  // measurement builds (tools/build_exp.sh) change this
 #endif
 constexpr uint32_t ENV_OWN_DRAWS_MIN = PBN_ENV_OWN_DRAWS_MIN;  // active lanes from which a wave skips the shared draw tables
+#ifndef PBN_HELP_SLEEP
+#define PBN_HELP_SLEEP 1  // a tail helper's sleep (x 64 cycles) between polls of its ring's consumed count
+#endif
 constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many updates are resolved longest-first
 
 // ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
@@ -1261,7 +1264,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                                     break;
                                 }
                                 if (jb < ldl(&rcw[8]) + ring_R) break;
-                                __builtin_amdgcn_s_sleep(1);
+                                __builtin_amdgcn_s_sleep(PBN_HELP_SLEEP);
                             }
                             if (stop) break;
                             uint32_t w4[4];
@@ -1463,21 +1466,36 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 // prefix), the first update that hits a cube, and the last writers' commits. The ring is read two
                 // blocks ahead: block j + 1's records are issued and block j + 2's slot polled while j resolves.
                 auto ring128 = [&]() {
-                    const uint4* const rs4 = reinterpret_cast<const uint4*>(ring_of(wv_in_wg));
+                    // wave-uniform column base (an SGPR, not a per-lane VGPR held across the loop) and the lane id
+                    // re-formed where it is used: the kernel is at its VGPR bound, and long-lived per-lane values in
+                    // this loop were spilled and reloaded from scratch on the block's chain
+                    const uint32_t cofs = __builtin_amdgcn_readfirstlane((uint32_t)(colb - lds));
+                    const uint8_t* const colr = lds + cofs;
+                    const uint32_t rofs = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint8_t*>(rcs) - lds));
+                    uint32_t* const rcr = reinterpret_cast<uint32_t*>(lds + rofs);  // the ring's control words (uniform)
+                    auto lane_now = [] {
+                        uint32_t v;
+                        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+                        return v;
+                    };
                     auto poll = [&](uint32_t jb, uint32_t sl) {
-                        if (ldl(&rcs[sl]) != jb) {
+                        if (ldl(&rcr[sl]) != jb) {
                             ++rwaits;  // diagnostics: the block's helper had not written it yet
-                            while (ldl(&rcs[sl]) != jb) __builtin_amdgcn_s_sleep(1);
+                            while (ldl(&rcr[sl]) != jb) __builtin_amdgcn_s_sleep(1);
                         }
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                        return rs4[sl * 64u + lane];
+                        // the slot's address from the control words' (the ring ends where they start), formed
+                        // here: a per-lane ring base held across the loop was spilled to scratch, putting a
+                        // scratch round trip between the tag and the slot read (stamps: 820 cycles of a 1,990 block)
+                        const uint32_t off = sl * 1024u + lane_now() * 16u;
+                        return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(rcr) - ring_R * 1024u + off);
                     };
                     auto nxt_slot = [&](uint32_t sl) { return sl + 1u == ring_R ? 0u : sl + 1u; };
                     auto nd_of = [&](const uint4& qq) { return *reinterpret_cast<const uint32_t*>(lds + (qq.w >> 16)); };
                     uint4 sC = poll(0u, 0u);
                     uint4 sN = poll(1u, nxt_slot(0u));
                     asm volatile("" ::"v"(sN.x), "v"(sN.w) : "memory");
-                    if (lane == 0) __hip_atomic_store(&rcs[8], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (lane == 0) __hip_atomic_store(&rcr[8], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     uint32_t rsl = nxt_slot(nxt_slot(0u));  // slot of block j + 2
                     uint4 qe = erec[sC.x & 0xFFFFu], qo = erec[sC.x >> 16];
                     uint32_t nde = nd_of(qe), ndo = nd_of(qo), inf = sC.y, rre = sC.z, rro = sC.w;
@@ -1494,14 +1512,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         uint32_t nround = 0;
 #endif
                         const uint32_t se = qe.z >> 24, so = qo.z >> 24;
-                        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(colb + (qe.x & 0xFFFFu));
-                        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(colb + (qe.x >> 16));
-                        const uint32_t e2 = *reinterpret_cast<const uint32_t*>(colb + (qe.y & 0xFFFFu));
-                        const uint32_t e3 = *reinterpret_cast<const uint32_t*>(colb + (qe.y >> 16));
-                        const uint32_t o0 = *reinterpret_cast<const uint32_t*>(colb + (qo.x & 0xFFFFu));
-                        const uint32_t o1 = *reinterpret_cast<const uint32_t*>(colb + (qo.x >> 16));
-                        const uint32_t o2 = *reinterpret_cast<const uint32_t*>(colb + (qo.y & 0xFFFFu));
-                        const uint32_t o3 = *reinterpret_cast<const uint32_t*>(colb + (qo.y >> 16));
+                        const uint32_t e0 = *reinterpret_cast<const uint32_t*>(colr + (qe.x & 0xFFFFu));
+                        const uint32_t e1 = *reinterpret_cast<const uint32_t*>(colr + (qe.x >> 16));
+                        const uint32_t e2 = *reinterpret_cast<const uint32_t*>(colr + (qe.y & 0xFFFFu));
+                        const uint32_t e3 = *reinterpret_cast<const uint32_t*>(colr + (qe.y >> 16));
+                        const uint32_t o0 = *reinterpret_cast<const uint32_t*>(colr + (qo.x & 0xFFFFu));
+                        const uint32_t o1 = *reinterpret_cast<const uint32_t*>(colr + (qo.x >> 16));
+                        const uint32_t o2 = *reinterpret_cast<const uint32_t*>(colr + (qo.y & 0xFFFFu));
+                        const uint32_t o3 = *reinterpret_cast<const uint32_t*>(colr + (qo.y >> 16));
                         // block j + 1's records, block j + 2's slot (in flight while this block resolves)
                         const uint4 qe2 = erec[sN.x & 0xFFFFu], qo2 = erec[sN.x >> 16];
                         const uint4 sNN = poll(jb + 2u, rsl);
@@ -1549,7 +1567,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
                         // block j + 2's slot is in registers: it is free (the asm keeps the store after the read)
                         asm volatile("" ::"v"(sNN.x), "v"(sNN.w) : "memory");
-                        if (lane == 0) __hip_atomic_store(&rcs[8], jb + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (lane == 0) __hip_atomic_store(&rcr[8], jb + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         rsl = nxt_slot(rsl);
                         // packed counter deltas in update order: the pair's sum prefixed over the lanes
                         const uint32_t sge = ye - 1u, sgo = yo - 1u;
@@ -1557,7 +1575,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         const uint32_t dodd = ((ndo & (0u - (yo ^ xo))) ^ sgo) - sgo;
                         const uint32_t pro = m + wave_inclusive_add(de + dodd), pre = pro - dodd;
                         const uint32_t nvalid = a.update_cap > u ? min(128u, a.update_cap - u) : 0u;
-                        const bool ve = 2u * lane < nvalid, vo = 2u * lane + 1u < nvalid;
+                        const uint32_t t2 = 2u * lane_now();  // this lane's even update
+                        const bool ve = t2 < nvalid, vo = t2 + 1u < nvalid;
                         // (no first-update test here: a ring starts 16 blocks into a session, u > 0)
                         const uint64_t SMe = __ballot(ve && has_zero_byte(pre) != 0u);
                         const uint64_t SMo = __ballot(vo && has_zero_byte(pro) != 0u);
@@ -1567,10 +1586,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         const uint32_t nd = ts < 256u ? ts + 1u : nvalid;
                         // commit: the last writer of each node among the first nd updates (both halves of a lane may
                         // write; nx says whether a later update of the prefix writes the same node)
-                        if (2u * lane < nd && nxe >= nd && ye != v3e)
-                            atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + (qe.y >> 16)), 1u << se);
-                        if (2u * lane + 1u < nd && nxo >= nd && yo != v3o)
-                            atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colb) + (qo.y >> 16)), 1u << so);
+                        if (t2 < nd && nxe >= nd && ye != v3e)
+                            atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colr) + (qe.y >> 16)), 1u << se);
+                        if (t2 + 1u < nd && nxo >= nd && yo != v3o)
+                            atomicXor(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(colr) + (qo.y >> 16)), 1u << so);
                         m = (uint32_t)__builtin_amdgcn_readlane((int)(((nd - 1u) & 1u) ? pro : pre), (int)((nd - 1u) >> 1));
                         u += nd;
                         hitf = ts < 256u;
