@@ -169,12 +169,15 @@ struct pbn_batch {
     int env_group = 0;        // PBNSIM_ENV_GROUP: lanes per env (1 = lane mode), 0 = by batch size
     int env_bpc = 0;          // PBNSIM_ENV_BPC: cap on resident workgroups per CU, 0 = none
     int env_chunk = 0;        // PBNSIM_ENV_CHUNK: draw-round chunk 32 / 48 of the cooperative-draw kernels, 0 = auto
-    int env_grid_cap = 0;     // PBNSIM_ENV_GRID: cap on the R6 kernel's workgroups (tests: lane refill), 0 = none
+    int env_grid_cap = 0;     // PBNSIM_ENV_GRID: the R6 kernel's workgroups (tests: lane refill, hand-offs), 0 = by size
     int env_tail = -1;        // PBNSIM_ENV_TAIL: the R6 kernel's tail-mode threshold (live envs per wave), -1 = default
     int env_lane_limit = 0;   // PBNSIM_ENV_LANES: lanes per wave taking envs in the tail-mode kernel, 0 = auto
     bool env_steal = true;    // PBNSIM_ENV_STEAL=0: no hand-off of tail envs between a workgroup's waves (k_env, mode 4)
     bool env_kernel_image = false;  // PBNSIM_ENV_KERNEL_IMAGE=1: k_env builds its LDS image (no host-built image)
     int env_helpers = 3;      // PBNSIM_ENV_HELPERS: at most this many tail helpers per session (0-3; 0 = off)
+    bool env_grid_steal = true;  // PBNSIM_ENV_GRID_STEAL=0: no grid-wide hand-off of tail envs (k_env, mode 4)
+    int env_grid_slots = 0;      // PBNSIM_ENV_GRID_SLOTS: pool slots in use (measurement: 1 keeps the waiting workgroups
+                                 // resident but moves at most one env), 0 = GPOOL_CAP
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
     bool ssd_serial = false;  // PBNSIM_SSD_SERIAL=1: wave mode applies each chunk serially (no chunk DAG)
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
@@ -205,6 +208,9 @@ struct pbn_batch {
     DevBuf s_counter;                                     // env-step work-queue head
     DevBuf s_steal;                                       // k_env tail hand-off: count of envs handed off
     bool steal_last = false;                              // the last R6 launch had the hand-off on
+    DevBuf s_gpool;                                       // k_env grid pool: control words, slot states, slots
+    uint32_t gpool_epoch = 0;                             // the last R6 launch's pool epoch
+    bool gpool_last = false;                              // the last R6 launch had the grid pool on
     PinBuf pin;                                           // staging for small host<->device copies
     DevBuf s_ssd_hist, s_ssd_tab;                         // SSD histogram + gap/target tables
     uint64_t ssd_iters = 0;                               // SSD iteration counter (Philox)
@@ -534,6 +540,8 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_STEAL")) b->env_steal = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = std::max(0, std::min(3, atoi(v)));
+    if (const char* v = getenv("PBNSIM_ENV_GRID_STEAL")) b->env_grid_steal = atoi(v) != 0;
+    if (const char* v = getenv("PBNSIM_ENV_GRID_SLOTS")) b->env_grid_slots = std::max(1, std::min((int)GPOOL_CAP, atoi(v)));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -584,7 +592,7 @@ void pbn_batch_destroy(pbn_batch* b) {
     if (b->d_error) (void)hipFree(b->d_error);
     for (DevBuf* d : {&b->s_act, &b->s_obs, &b->s_rew, &b->s_flags, &b->s_nup, &b->s_replay_i, &b->s_replay_k,
                       &b->s_off, &b->s_mask, &b->mt_py, &b->mt_np, &b->mt_pos_py, &b->mt_pos_np, &b->mt_seeds,
-                      &b->s_counter, &b->s_steal, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase, &b->s_flip_err})
+                      &b->s_counter, &b->s_steal, &b->s_gpool, &b->s_ssd_hist, &b->s_ssd_tab, &b->s_sync_tab, &b->s_ubase, &b->s_flip_err})
         d->release();
     for (hipGraphExec_t& g : b->step_graph)
         if (g) (void)hipGraphExecDestroy(g);
@@ -1536,7 +1544,9 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     HIP_TRY(hipMemsetAsync(b->s_counter.p, 0, 8, b->stream));
     // lanes per env (group mode) or, with a lane limit, 64 / limit lane slots per env
     int grid = b->grid_for(a.lane_limit < 64u ? (b->B * 64u + a.lane_limit - 1u) / a.lane_limit : b->B * (uint64_t)grp, bpc);
-    if (b->env_grid_cap) grid = std::min(grid, b->env_grid_cap);  // persistent waves: any grid drains the counter
+    // PBNSIM_ENV_GRID: exactly that many workgroups (at most the resident count; persistent waves: any grid
+    // drains the counter, and surplus workgroups find the queue empty)
+    if (b->env_grid_cap) grid = std::min(b->env_grid_cap, b->n_cu * bpc);
     // tail hand-off (k_env mode 4): a wave holding several envs in tail mode passes envs it has not
     // started on to idle waves of its workgroup (LDS). One lane per wave taking envs (small batches)
     // never holds two: off there
@@ -1550,6 +1560,25 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         a.steal_count = (uint32_t*)b->s_steal.p;
         a.tail_helpers = b->env_helpers;
         b->steal_last = true;
+        // grid pool: control words (GPOOL_CTL_BYTES, zeroed per launch), then the slots' state words, then the slots
+        b->gpool_last = false;
+        if (b->env_grid_steal) {
+            const size_t st_bytes = 4 * (size_t)GPOOL_CAP, sl_bytes = 8 * (size_t)GPOOL_GRANULES * GPOOL_CAP;
+            if (int rc = b->s_gpool.ensure(GPOOL_CTL_BYTES + st_bytes + sl_bytes)) return rc;
+            HIP_TRY(hipMemsetAsync(b->s_gpool.p, 0, GPOOL_CTL_BYTES, b->stream));
+            uint8_t* base = static_cast<uint8_t*>(b->s_gpool.p);
+            // epochs 1 .. 2^30 - 1: slot words of earlier launches never match; the whole pool is zeroed at its
+            // first use and when the epoch wraps
+            if (b->gpool_epoch == 0u || b->gpool_epoch >= 0x3FFFFFFEu)
+                HIP_TRY(hipMemsetAsync(base, 0, GPOOL_CTL_BYTES + st_bytes + sl_bytes, b->stream));
+            b->gpool_epoch = b->gpool_epoch % 0x3FFFFFFEu + 1u;
+            a.gpool_ctl = reinterpret_cast<uint32_t*>(base);
+            a.gpool_state = reinterpret_cast<uint32_t*>(base + GPOOL_CTL_BYTES);
+            a.gpool = reinterpret_cast<uint64_t*>(base + GPOOL_CTL_BYTES + st_bytes);
+            a.gpool_cap = b->env_grid_slots > 0 ? (uint32_t)b->env_grid_slots : GPOOL_CAP;
+            a.gpool_epoch = b->gpool_epoch;
+            b->gpool_last = true;
+        }
     }
     hipEvent_t stop;
     if (int rc = b->ev_begin(&stop)) return rc;
@@ -1594,6 +1623,7 @@ static int env_host_out(pbn_batch* b, uint64_t* obs, int32_t* reward, uint8_t* f
         if (n_updates) memcpy(n_updates, q + on, sn);
         int32_t err;
         memcpy(&err, q + oe, 4);
+        if (err & 2) return fail(PBN_E_HIP, "k_env grid pool: a wait timed out");
         if (err) return fail(PBN_E_RANGE, "an action was out of range");
         return 0;
     }
@@ -1604,6 +1634,7 @@ static int env_host_out(pbn_batch* b, uint64_t* obs, int32_t* reward, uint8_t* f
     int32_t err = 0;
     HIP_TRY(hipMemcpyAsync(&err, b->d_error, 4, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    if (err & 2) return fail(PBN_E_HIP, "k_env grid pool: a wait timed out");
     if (err) return fail(PBN_E_RANGE, "an action was out of range");
     return 0;
 }
@@ -1752,6 +1783,22 @@ int pbn_env_tail_stats(pbn_batch* b, uint32_t* stats) {
     if (!b->steal_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
     HIP_TRY(hipMemcpy(stats, b->s_steal.p, 16, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int pbn_env_grid_stats(pbn_batch* b, uint32_t* stats) {
+    CHECK_NN(b, "batch");
+    CHECK_NN(stats, "stats");
+    SET_DEV(b);
+    for (int k = 0; k < 4; k++) stats[k] = 0;
+    if (!b->gpool_last) return 0;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    uint32_t ctl[5];
+    HIP_TRY(hipMemcpy(ctl, b->s_gpool.p, sizeof ctl, hipMemcpyDeviceToHost));
+    stats[0] = ctl[3];  // envs pushed
+    stats[1] = ctl[1];  // tickets taken
+    stats[2] = ctl[4];  // waits given up
+    stats[3] = ctl[2];  // live count at the end (0 after a complete launch)
     return 0;
 }
 

@@ -587,6 +587,13 @@ constexpr uint32_t ENV_OWN_DRAWS_MIN = PBN_ENV_OWN_DRAWS_MIN;  // active lanes f
 #define PBN_HELP_SLEEP 1  // a tail helper's sleep (x 64 cycles) between polls of its ring's consumed count
 #endif
 constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many updates are resolved longest-first
+// grid pool (k_env): global-address-space views, so agent-scope atomics lower to global_ (not flat_) sc1 accesses
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+#ifndef PBN_GPOOL_CHECK_TICKS
+#define PBN_GPOOL_CHECK_TICKS 500  // a tail wave looks for waiting workgroups at most every 5 us (100 MHz ticks)
+#endif
+constexpr uint64_t GPOOL_TIMEOUT_TICKS = 200000000ull;  // 2 s: a ticket holder gives up (error flag 2; never expected)
 
 // ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
 struct RankMagic {
@@ -687,9 +694,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     const uint32_t CH = GEN ? a.chunk : ENV_CHUNK;
     const uint32_t GWB = env_gen_wave_bytes(CH);
     uint32_t* const wctl = reinterpret_cast<uint32_t*>(lds + a.off_gen + (BLOCK / 64) * GWB);
+    // grid pool words: device memory, every access a global agent-scope atomic (sc1: past the CU's L1)
+    auto gctl = [&](int k) { return (gu32*)(a.gpool_ctl + k); };
+    const bool GRID = TAIL && a.steal_local && a.gpool_cap != 0u;
     if (TAIL && a.steal_local && threadIdx.x == 0) {
         wctl[0] = BLOCK / 64;  // busy
         wctl[1] = 0u;          // idle mask
+        wctl[2] = 0u;          // grid pool: a wave of this workgroup is waiting on a ticket
+        wctl[3] = 0u;          // grid pool: 1 the launch's work is done, leave; 2 this workgroup left its CU's count
+        if (GRID) {
+            // this workgroup counts as live from its start (a workgroup dispatched late counts from then: a
+            // ticket holder that saw the count at 0 gave its slot up, so no env can be pushed to it), and as
+            // working on its CU until it first runs out of work
+            (void)__hip_atomic_fetch_add(gctl(2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            (void)__hip_atomic_fetch_add(gctl(GPOOL_CU_WORD + __smid()), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
     __syncthreads();
     const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes + a.erec_shift) + threadIdx.x};
@@ -776,8 +796,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     // ring blocks are 128 updates (two per lane: 16 B per lane, 1 KiB per slot). The ring may run over the
     // session wave's own hand-off flag and box: those are unused while it is in a session (it clears its flag
     // before it next goes idle). Helpers keep a 128-bit writer-mask table (2 x wm_bytes) below their own flag.
-    const uint32_t ring_R = (GWB > wm_bytes + 80u && 2u * wm_bytes <= CH * 128u)
-                                ? min(8u, (GWB - wm_bytes - 80u) / 1024u) : 0u;
+    // (the ring's control words end at least 24 B before the draw buffer's end: the grid pool's view is there)
+    const uint32_t ring_R = (GWB > wm_bytes + 96u && 2u * wm_bytes <= CH * 128u)
+                                ? min(8u, (GWB - wm_bytes - 96u) / 1024u) : 0u;
     auto ring_of = [&](uint32_t w) { return lds + a.off_gen + w * GWB + wm_bytes; };
     auto rctl_of = [&](uint32_t w) { return reinterpret_cast<uint32_t*>(ring_of(w) + ring_R * 1024u); };
     constexpr uint64_t HELP_MARK = 0xFFFFFFFFFFFFFFFEull;  // box[0] of a wave recruited as a helper
@@ -822,6 +843,152 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 #endif
         }
     };
+    // ---- grid pool: the same hand-off between workgroups. A workgroup whose waves have all run out of work
+    // takes a ticket (one wave waits on it for the workgroup); a tail wave that still holds envs it has not
+    // started on after the workgroup hand-off, and sees tickets nobody has filled, reserves that many slots
+    // and writes one env into each -- the hand-off box's words as 8-B {epoch, value} granules, each one
+    // aligned write-through store, so a slot is complete when every granule carries this launch's epoch (no
+    // flag, no fence; MI355X_MICROARCH.md "granules"). A slot is claimed by an atomic max on its state word
+    // (epoch << 2 | 1) before it is written; a ticket holder that finds the live count at 0 (no workgroup
+    // working, no env in the pool) gives its slot up by a max to epoch << 2 | 2 -- whichever lands first
+    // tells the other (a late push sees the slot given up and keeps its env; a holder that sees it claimed
+    // waits for the granules). Epochs only grow between the pool's zeroings, so older states never match.
+    // The waiting wave's siblings stay idle in LDS, so an env received this way gets tail helpers too.
+    // Bit-exact like the workgroup hand-off: an env's draws are keyed by its global id, not by the wave.
+    constexpr uint32_t NBW = 2u * (5u + 2u * (uint32_t)W);  // hand-off words (u32) per env
+    static_assert(NBW <= GPOOL_GRANULES && NBW <= 64u, "grid pool slot: one granule per lane");
+    const uint32_t GE = a.gpool_epoch & 0x3FFFFFFFu;
+    // The pool as this wave last saw it -- [0] tickets taken, [1] slots reserved, loaded into LDS by an
+    // asynchronous LDS-DMA load (global_load_lds, sc1) issued at the previous look, so looking costs no round
+    // trip -- and [2] the realtime (low 32 bits) before which the wave does not look again: the last 12 B of its
+    // draw buffer (past the ring's control words; unused in tail mode, where the view lives)
+    uint32_t* const gview = reinterpret_cast<uint32_t*>(lds + a.off_gen + wv_in_wg * GWB + GWB - 12u);
+    auto gview_issue = [&]() {
+        if (lane < 2u)
+            __builtin_amdgcn_global_load_lds((gu32*)(a.gpool_ctl + 1u - lane),
+                                             (__attribute__((address_space(3))) uint32_t*)gview, 4, 0, 16);
+    };
+    auto grid_push = [&](uint64_t cand) {
+        if constexpr (TAIL) {
+            if (!GRID || cand == 0ull) return;
+            const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            if ((int32_t)(now - gview[2]) < 0) return;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the view loaded at the last look has landed
+            const int32_t waiting = (int32_t)(gview[0] - gview[1]);
+            wave_sync();
+            if (lane == 0) gview[2] = now + PBN_GPOOL_CHECK_TICKS;
+            gview_issue();  // for the next look
+            if (waiting <= 0) return;
+            // one env (the lowest lane of cand): lane 0 reserves a slot and claims it (atomic max of the slot's
+            // state: a ticket holder that gave the slot up raised it past this value first); the env's words go
+            // through this wave's own hand-off box (unused while it works), then one granule per lane
+            int ok = 0;
+            uint32_t sl = 0;
+            if (lane == 0) {
+                (void)__hip_atomic_fetch_add(gctl(2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // live first
+                sl = __hip_atomic_fetch_add(gctl(0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (sl < a.gpool_cap)
+                    ok = (__hip_atomic_fetch_max((gu32*)(a.gpool_state + sl), GE << 2 | 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE;
+                // given up by its ticket holder, or past the pool: the env stays here
+                (void)__hip_atomic_fetch_add(ok ? gctl(3) : gctl(2), ok ? 1u : 0xFFFFFFFFu, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (!__shfl(ok, 0)) return;
+            sl = (uint32_t)__shfl((int)sl, 0);
+            uint64_t* box = box_of(wv_in_wg);
+            if (lane == (uint32_t)__ffsll((unsigned long long)cand) - 1u) {
+                uint64_t s[W];
+                from_plane<W>(P, s);
+                box[0] = (uint64_t)e;
+                box[1] = (uint64_t)nst;
+                box[2] = (uint64_t)t | (uint64_t)used << 32;
+                box[3] = (uint64_t)m_lo | (hit0 ? 1ull << 32 : 0ull);
+                box[4] = (uint64_t)(int64_t)n_act;
+#pragma unroll
+                for (int k2 = 0; k2 < W; ++k2) {
+                    box[5 + k2] = o0[k2];
+                    box[5 + W + k2] = s[k2];
+                }
+                e = -1;
+                exhausted = true;
+            }
+            wave_sync();
+            if (lane < NBW) {
+                const uint32_t v = reinterpret_cast<const uint32_t*>(box)[lane];
+                __hip_atomic_store((gu64*)(a.gpool + (uint64_t)sl * GPOOL_GRANULES) + lane,
+                                   (unsigned long long)GE << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            wave_sync();  // the box's reads are done before anything reuses it
+        }
+    };
+    // The workgroup's waiting wave (whole wave): a ticket, then its slot's granules swept until every one
+    // carries this launch's epoch (true: the env's words are in this wave's box), or the launch is done
+    // (false). The workgroup stops counting as live when it takes the ticket.
+    // Only a workgroup whose CU has no workgroup still on its own envs takes a ticket: an env moved onto a CU
+    // where other waves still work would slow the waves the launch is waiting for (measured: cap 4,096 per
+    // step 1.15 -> 1.34 ms when any idle workgroup took envs), while a finished workgroup there leaves the CU
+    // to them. Until then it waits (or leaves when nothing is live).
+    auto grid_pop = [&]() -> bool {
+        uint32_t ticket = 0;
+        int leave = 0;
+        if (lane == 0) {
+            (void)__hip_atomic_fetch_add(gctl(2), 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gu32* cu = gctl(GPOOL_CU_WORD + __smid());
+            if ((ldl(&wctl[3]) & 2u) == 0u) {  // the first time this workgroup runs out of work
+                __hip_atomic_store(&wctl[3], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                (void)__hip_atomic_fetch_add(cu, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            while (__hip_atomic_load(cu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                if (__hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                    leave = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(32);
+            }
+            if (!leave) ticket = __hip_atomic_fetch_add(gctl(1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (__shfl(leave, 0)) return false;
+        ticket = (uint32_t)__shfl((int)ticket, 0);
+        const bool has_slot = ticket < a.gpool_cap;
+        gu64* g = (gu64*)(a.gpool + (uint64_t)(has_slot ? ticket : 0u) * GPOOL_GRANULES);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t it = 0;; ++it) {
+            // lane 0 polls the slot's last granule; once it carries the epoch, the whole wave sweeps the slot
+            int seen = 0;
+            if (lane == 0 && has_slot)
+                seen = (uint32_t)(__hip_atomic_load(g + (NBW - 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == GE;
+            if (__shfl(seen, 0)) {
+                for (;;) {
+                    uint64_t x = 0;
+                    if (lane < NBW) x = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__ballot(lane < NBW && (uint32_t)(x >> 32) != GE) == 0ull) {
+                        if (lane < NBW) reinterpret_cast<uint32_t*>(box_of(wv_in_wg))[lane] = (uint32_t)x;
+                        wave_sync();
+                        return true;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            if ((it & 1u) == 1u) {
+                int leave = 0;
+                if (lane == 0) {
+                    if (__hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                        // nothing live: no push can come any more -- unless one already claimed this slot
+                        leave = !has_slot || (__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u,
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE;
+                    }
+                    if (!leave && __builtin_amdgcn_s_memrealtime() - t0 > GPOOL_TIMEOUT_TICKS) {
+                        leave = 1;
+                        (void)__hip_atomic_fetch_add(gctl(4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        atomicOr(a.error, 2);
+                    }
+                }
+                if (__shfl(leave, 0)) return false;
+            }
+            __builtin_amdgcn_s_sleep(32);
+        }
+    };
     auto local_pop = [&]() -> int {  // 0: leave, 1: an env in lane 0, 2: a helper request (help_req)
         if constexpr (TAIL) {
 #ifdef PBN_STAMPS
@@ -843,19 +1010,62 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                         break;
                     }
                     if (ldl(&wctl[0]) == 0u) {
-                        // nobody busy: leave, unless a pusher claimed this wave before the count reached 0
-                        if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
-                            got = -1;
+                        if (GRID) {
+                            // nobody busy: the launch is done (the waiting wave said so) -- leave with the idle
+                            // bit set (no wave is busy to claim it); else one wave waits on a ticket for the
+                            // workgroup (the others stay idle here)
+                            if (ldl(&wctl[3]) & 1u) {
+                                got = -1;
+                                break;
+                            }
+                            uint32_t zero = 0u;
+                            if (__hip_atomic_compare_exchange_strong(&wctl[2], &zero, 1u, __ATOMIC_RELAXED,
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                                if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
+                                    bit) {
+                                    got = 3;
+                                    break;
+                                }
+                                // claimed meanwhile: an env or a helper request is on its way
+                                __hip_atomic_store(&wctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                while (ldl(flag_of(wv_in_wg)) == 0u) __builtin_amdgcn_s_sleep(1);
+                                got = 1;
+                                break;
+                            }
+                            // a sibling waits on the pool: nothing can arrive here until it has an env, so poll
+                            // slowly (this CU's other workgroups may still be working)
+                            __builtin_amdgcn_s_sleep(30);
+                        } else {
+                            // nobody busy: leave, unless a pusher claimed this wave before the count reached 0
+                            if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {
+                                got = -1;
+                                break;
+                            }
+                            while (ldl(flag_of(wv_in_wg)) == 0u) __builtin_amdgcn_s_sleep(1);
+                            got = 1;
                             break;
                         }
-                        while (ldl(flag_of(wv_in_wg)) == 0u) __builtin_amdgcn_s_sleep(1);
-                        got = 1;
-                        break;
                     }
                     __builtin_amdgcn_s_sleep(2);
                 }
             }
             got = __shfl(got, 0);
+            if (got == 3) {  // this wave waits on the grid pool for the workgroup
+                const bool env = grid_pop();
+                if (lane == 0) {
+                    if (env) {
+                        // busy before the ticket word is released: the siblings never see the workgroup idle
+                        (void)__hip_atomic_fetch_add(&wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&wctl[2], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        (void)__hip_atomic_fetch_or(&wctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                got = env ? 1 : -1;
+#ifdef PBN_STAMPS
+                est[16] += env ? 0x10000u : 0u;  // envs received from the grid pool (high half)
+#endif
+            }
 #ifdef PBN_STAMPS
             est[17] += __builtin_amdgcn_s_memrealtime() - t_in;
             est[15] += got > 0 ? 1u : 0u;
@@ -1020,6 +1230,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 uint64_t* wm = reinterpret_cast<uint64_t*>(lds + a.off_gen + (threadIdx.x >> 6) * GWB);
                 if (!tmode) {
                     for (uint32_t k = lane; k < wm_bytes / 8u; k += 64) wm[k] = 0ull;
+                    if (GRID) {  // the pool's view: first look after PBN_GPOOL_CHECK_TICKS, its load issued now
+                        if (lane == 0) gview[2] = (uint32_t)__builtin_amdgcn_s_memrealtime() + PBN_GPOOL_CHECK_TICKS;
+                        wave_sync();
+                        gview_issue();
+                    }
                     wave_sync();
                     tmode = true;
                 }
@@ -1035,7 +1250,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                             (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_max(e >= 0 ? used : 0u), 63);
                         L = (uint32_t)__ffsll((unsigned long long)__ballot(e >= 0 && used == mx)) - 1u;
                     }
-                    if (a.steal_local && (act & ~(1ull << L)) != 0ull) local_push(act & ~(1ull << L));
+                    if (a.steal_local && (act & ~(1ull << L)) != 0ull) {
+                        local_push(act & ~(1ull << L));
+                        grid_push(__ballot(e >= 0) & ~(1ull << L));  // what the workgroup could not take
+                    }
                 }
                 // the env's registers from lane L (wave-uniform index: v_readlane, no LDS permute); a helper
                 // takes the session's update base, call index and env id from the session wave's ring control
@@ -1422,7 +1640,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     // ring blocks (the self-prepared block k + 1 in D is dropped)
                     if (a.steal_local && (++nblk & 15u) == 0u && !fin) {
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
-                        if (others) local_push(others);
+                        if (others) {
+                            local_push(others);
+                            grid_push(__ballot(e >= 0) & ~(1ull << L));
+                        }
                         if (SPLIT && a.tail_helpers && ring_R >= 3u && ldl(&wctl[1]) != 0u) {
                             const uint32_t cl = claim_idle(min((uint32_t)a.tail_helpers, 3u));
                             if (cl) {

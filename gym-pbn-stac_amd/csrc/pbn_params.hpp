@@ -124,7 +124,22 @@ struct EnvArgs {
     int32_t tail_helpers;     // fast == 4 (with steal_local): up to this many (<= 3) idle waves of the workgroup prepare a long tail
                               // session's blocks ahead (draws, records, writer masks) into the session wave's
                               // LDS ring, so the session wave only resolves (k_env, tail helpers)
+    // fast == 4 (with steal_local): grid-wide hand-off of tail envs to workgroups that have run out of work
+    // (k_env, "grid pool"). Device memory, control words zeroed per launch:
+    uint32_t* gpool_ctl;      // [0] slots reserved by pushers, [1] tickets taken by idle workgroups, [2] live:
+                              // workgroups working + envs in the pool, [3] envs pushed, [4] waits given up
+    uint32_t* gpool_state;    // [gpool_cap] per slot: epoch << 2 | 1 (a pusher claimed it) or | 2 (its ticket
+                              // holder gave up on it); any other epoch: unclaimed
+    uint64_t* gpool;          // [gpool_cap][GPOOL_GRANULES] 8-B {epoch, value} granules: one env's hand-off words
+    uint32_t gpool_cap;       // slots; 0 = grid hand-off off
+    uint32_t gpool_epoch;     // this launch's tag (1 .. 2^30 - 1, a new one per launch)
 };
+
+constexpr uint32_t GPOOL_GRANULES = 64;  // per slot: the hand-off box as u32 words (10 + 4W <= 64 for W <= 13)
+constexpr uint32_t GPOOL_CAP = 8192;     // grid pool slots (4 MiB); envs past them stay with their wave
+// control words: [0, 16) counters, [GPOOL_CU_WORD + __smid()] workgroups on that CU still on their own envs
+// (__smid() < 1024: XCC, SE, CU id bits); the block is zeroed per launch
+constexpr uint32_t GPOOL_CU_WORD = 16, GPOOL_CTL_BYTES = 4u * (GPOOL_CU_WORD + 1024u);
 
 constexpr uint32_t MT_ROW = 624;
 

@@ -128,6 +128,7 @@ SIGNATURES = {
     "pbn_env_handoffs": (C.c_int, [_vp, _u32p]),
     "pbn_env_tail_helpers": (C.c_int, [_vp, _u32p]),
     "pbn_env_tail_stats": (C.c_int, [_vp, _u32p]),
+    "pbn_env_grid_stats": (C.c_int, [_vp, _u32p]),
 }
 
 

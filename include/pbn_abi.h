@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 12
+#define PBN_ABI_VERSION 13
 
 enum {
     PBN_OK = 0,
@@ -141,7 +141,9 @@ int pbn_net_select_u32(const pbn_net *net, int32_t node, uint32_t a, uint64_t *r
 /* ---- batches of independent envs (the reference holds one Graph per env) ---- */
 /* Tuning knobs, read from the environment once here (measurement and tests only):
  * PBNSIM_STORE_MODE, PBNSIM_ENVS_PER_THREAD, PBNSIM_STEP_BLOCK (step kernel);
- * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC (R6 env kernel); PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL, PBNSIM_SSD_SHARED (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
+ * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC, PBNSIM_ENV_CHUNK, PBNSIM_ENV_GRID, PBNSIM_ENV_TAIL,
+ * PBNSIM_ENV_LANES, PBNSIM_ENV_STEAL, PBNSIM_ENV_HELPERS, PBNSIM_ENV_GRID_STEAL, PBNSIM_ENV_KERNEL_IMAGE (R6 env kernel);
+ * PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL, PBNSIM_SSD_SHARED (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
  * PBNSIM_STEP_GRAPH=0 (pbn_step without HIP graphs). */
 int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
                      pbn_batch **out);
@@ -263,6 +265,11 @@ int pbn_env_tail_helpers(pbn_batch *b, uint32_t *count);
  * sessions read from their helpers' rings, and of those the blocks not yet written when the session reached
  * them (the session waited). Syncs the batch stream. Diagnostics. */
 int pbn_env_tail_stats(pbn_batch *b, uint32_t *stats);
+/* The last R6 launch's grid-pool counters, stats[4] (env_kernel 4 with the hand-off on; PBNSIM_ENV_GRID_STEAL=0
+ * turns the pool off): envs a tail wave handed to a workgroup that had run out of work (anywhere on the GPU),
+ * tickets those workgroups took, waits given up (0 unless a launch failed with PBN_E_HIP), and the live count
+ * at the launch's end (0). Syncs the batch stream. Diagnostics. */
+int pbn_env_grid_stats(pbn_batch *b, uint32_t *stats);
 
 #ifdef __cplusplus
 }

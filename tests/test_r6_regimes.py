@@ -345,7 +345,7 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
     b.close()
 
 
-@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off"])
+@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off", "grid", "grid_off"])
 @pytest.mark.parametrize("mode", ["per_step", "fused"])
 def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypatch, mode, case):
     """A case in which the workgroup hand-off must happen: one workgroup (4 waves), two
@@ -358,13 +358,23 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     ``helpers``: 2 envs, both taken by one wave (two lanes); at its 16-block re-check it hands its
     unstarted env to an idle wave and recruits the other idle waves as tail helpers, which prepare its
     blocks (draws, records, writer masks) into its LDS ring while it resolves them (asserted: helpers
-    recruited; exact against the oracle). ``helpers_off``: the same with PBNSIM_ENV_HELPERS=0 (none)."""
+    recruited; exact against the oracle). ``helpers_off``: the same with PBNSIM_ENV_HELPERS=0 (none).
+
+    ``grid``: the grid pool (k_env, EnvArgs::gpool) -- two workgroups, 16 lanes per wave taking envs, 16
+    envs: the first wave to reach the work queue takes all of them, every other wave of both workgroups
+    goes idle, so the other workgroup waits on a ticket while the loaded wave, after handing three envs
+    to its idle siblings, still holds unstarted ones: it pushes envs into the pool (asserted) and the
+    waiting workgroup resumes them; every output equals the oracle. ``grid_off``: PBNSIM_ENV_GRID_STEAL=0
+    (nothing pushed)."""
     import torch
 
-    monkeypatch.setenv("PBNSIM_ENV_LANES", "2")
-    monkeypatch.setenv("PBNSIM_ENV_GRID", "1")
+    grid_case = case.startswith("grid")
+    monkeypatch.setenv("PBNSIM_ENV_LANES", "16" if grid_case else "2")
+    monkeypatch.setenv("PBNSIM_ENV_GRID", "2" if grid_case else "1")
     if case == "helpers_off":
         monkeypatch.setenv("PBNSIM_ENV_HELPERS", "0")
+    if case == "grid_off":
+        monkeypatch.setenv("PBNSIM_ENV_GRID_STEAL", "0")
     import sys
     from pathlib import Path
 
@@ -378,7 +388,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
                 horizon=100)
     o = oracle_mod.Oracle(net)
-    B, seed, base, T, A, cap = (6 if case == "handoff" else 2), 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
+    B, seed, base, T, A, cap = (6 if case == "handoff" else 16 if grid_case else 2), 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     # per env, the first candidate action row (oracle) whose first env step runs >= 2,048 updates
@@ -399,7 +409,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     assert np.array_equal(b.get_state(), st)
-    handed, helpers = [], []
+    handed, helpers, pool = [], [], []
     if mode == "fused":
         dev = torch.device("cuda", 0)
         d_a = torch.from_numpy(acts).to(dev)
@@ -412,6 +422,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
         b.sync()
         handed.append(b.env_handoffs())
         helpers.append(b.env_tail_helpers())
+        pool.append(b.env_grid_stats())
         got = [(o_[t].cpu().numpy().view(np.uint64), r_[t].cpu().numpy(), f_[t].cpu().numpy(),
                 n_[t].cpu().numpy().view(np.uint32)) for t in range(T)]
     else:
@@ -420,10 +431,17 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
             got.append(b.env_step_multi(cfg, acts[t], update_cap=cap))
             handed.append(b.env_handoffs())
             helpers.append(b.env_tail_helpers())
+            pool.append(b.env_grid_stats())
     info = b.info()
-    assert info["env_kernel"] == 4 and info["env_lane_limit"] == 2 and info["env_grid"] == 1
+    assert info["env_kernel"] == 4 and info["env_lane_limit"] == (16 if grid_case else 2)
+    assert info["env_grid"] == (2 if grid_case else 1)
     assert info["env_handoff"] == 1
     assert handed[0] > 0, handed  # the first launch (every env long) must hand off
+    assert all(p["gave_up"] == 0 and p["live_at_end"] == 0 for p in pool), pool
+    if case == "grid":
+        assert pool[0]["pushed"] > 0, pool  # ... and push envs to the waiting workgroup
+    if case == "grid_off":
+        assert sum(p["pushed"] + p["tickets"] for p in pool) == 0, pool
     if case == "helpers":
         assert helpers[0] > 0, helpers  # ... and recruit the remaining idle waves as helpers
     if case == "helpers_off":

@@ -104,10 +104,16 @@ def main():
         # tail hand-off between a workgroup's waves (k_env mode 4, EnvArgs::steal_local): per wave envs
         # received / handed off, time spent idle waiting for one, first time idle
         pct = lambda v: {f"p{q}": round(float(np.percentile(v, q)), 1) for q in (0, 10, 50, 90, 100)}
-        res["handoff"] = {"envs_received": pct(st[:, 15]), "envs_pushed": pct(st[:, 16]),
-                          "total_received": int(st[:, 15].sum()), "total_pushed": int(st[:, 16].sum()),
+        res["handoff"] = {"envs_received": pct(st[:, 15]), "envs_pushed": pct(st[:, 16] & 0xFFFF),
+                          "total_received": int(st[:, 15].sum()), "total_pushed": int((st[:, 16] & 0xFFFF).sum()),
                           "idle_wait_us": pct(st[:, 17] / 100.0),
                           "first_idle_us": pct((st[st[:, 18] > 0, 18] - t0) / 100.0) if (st[:, 18] > 0).any() else None}
+        lt = st[:, 35] > 0  # the wave's last tail block's end (realtime)
+        res["last_tail_block_end_us"] = pct((st[lt, 35] - t0) / 100.0) if lt.any() else None
+        res["envs_from_grid_pool"] = int((st[:, 16] >> 16).sum())
+        res["tail_blocks"] = int(st[:, 19].sum())
+        res["tail_block_us_mean"] = round(float(st[:, 32].sum() / max(st[:, 19].sum(), 1) / 100.0), 4)
+        res["tail_block_rounds_mean"] = round(float(st[:, 21].sum() / max(st[:, 19].sum(), 1)), 3)
         res["chunks_per_wave_p50"] = float(np.median(st[:, 8]))
         res["mean_active_lanes_per_chunk_p50"] = float(np.median(st[:, 9] / np.maximum(st[:, 8], 1)))
         out["reps"].append(res)
