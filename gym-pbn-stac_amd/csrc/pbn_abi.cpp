@@ -175,7 +175,10 @@ struct pbn_batch {
     bool env_steal = true;    // PBNSIM_ENV_STEAL=0: no hand-off of tail envs between a workgroup's waves (k_env, mode 4)
     bool env_kernel_image = false;  // PBNSIM_ENV_KERNEL_IMAGE=1: k_env builds its LDS image (no host-built image)
     int env_helpers = 3;      // PBNSIM_ENV_HELPERS: at most this many tail helpers per session (0-3; 0 = off)
-    bool env_grid_steal = true;  // PBNSIM_ENV_GRID_STEAL=0: no grid-wide hand-off of tail envs (k_env, mode 4)
+    // PBNSIM_ENV_GRID_STEAL: grid-wide hand-off of tail envs (k_env, mode 4): 1 on, 0 off, unset = fused launches
+    // and update caps from GPOOL_MIN_CAP (below it one env step's loops are too short to repay the waiting
+    // workgroups' residency)
+    int env_grid_steal = -1;
     int env_grid_slots = 0;      // PBNSIM_ENV_GRID_SLOTS: pool slots in use (measurement: 1 keeps the waiting workgroups
                                  // resident but moves at most one env), 0 = GPOOL_CAP
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
@@ -540,7 +543,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_STEAL")) b->env_steal = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = std::max(0, std::min(3, atoi(v)));
-    if (const char* v = getenv("PBNSIM_ENV_GRID_STEAL")) b->env_grid_steal = atoi(v) != 0;
+    if (const char* v = getenv("PBNSIM_ENV_GRID_STEAL")) b->env_grid_steal = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("PBNSIM_ENV_GRID_SLOTS")) b->env_grid_slots = std::max(1, std::min((int)GPOOL_CAP, atoi(v)));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
@@ -1562,7 +1565,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         b->steal_last = true;
         // grid pool: control words (GPOOL_CTL_BYTES, zeroed per launch), then the slots' state words, then the slots
         b->gpool_last = false;
-        if (b->env_grid_steal) {
+        if (b->env_grid_steal > 0 || (b->env_grid_steal < 0 && (cap >= GPOOL_MIN_CAP || n_calls > 1u))) {
             const size_t st_bytes = 4 * (size_t)GPOOL_CAP, sl_bytes = 8 * (size_t)GPOOL_GRANULES * GPOOL_CAP;
             if (int rc = b->s_gpool.ensure(GPOOL_CTL_BYTES + st_bytes + sl_bytes)) return rc;
             HIP_TRY(hipMemsetAsync(b->s_gpool.p, 0, GPOOL_CTL_BYTES, b->stream));

@@ -590,6 +590,9 @@ constexpr uint32_t ENV_LONG_USED = 1024;  // tail mode: envs past this many upda
 // grid pool (k_env): global-address-space views, so agent-scope atomics lower to global_ (not flat_) sc1 accesses
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+#ifndef PBN_GPOOL_SLEEP
+#define PBN_GPOOL_SLEEP 32  // a workgroup waiting on the pool sleeps this x 64 cycles between polls
+#endif
 #ifndef PBN_GPOOL_CHECK_TICKS
 #define PBN_GPOOL_CHECK_TICKS 500  // a tail wave looks for waiting workgroups at most every 5 us (100 MHz ticks)
 #endif
@@ -944,7 +947,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     leave = 1;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(32);
+                __builtin_amdgcn_s_sleep(PBN_GPOOL_SLEEP);
             }
             if (!leave) ticket = __hip_atomic_fetch_add(gctl(1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -986,7 +989,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 }
                 if (__shfl(leave, 0)) return false;
             }
-            __builtin_amdgcn_s_sleep(32);
+            __builtin_amdgcn_s_sleep(PBN_GPOOL_SLEEP);
         }
     };
     auto local_pop = [&]() -> int {  // 0: leave, 1: an env in lane 0, 2: a helper request (help_req)
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                             }
                             // a sibling waits on the pool: nothing can arrive here until it has an env, so poll
                             // slowly (this CU's other workgroups may still be working)
-                            __builtin_amdgcn_s_sleep(30);
+                            __builtin_amdgcn_s_sleep(PBN_GPOOL_SLEEP);
                         } else {
                             // nobody busy: leave, unless a pusher claimed this wave before the count reached 0
                             if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit) {

@@ -140,6 +140,10 @@ constexpr uint32_t GPOOL_CAP = 8192;     // grid pool slots (4 MiB); envs past t
 // control words: [0, 16) counters, [GPOOL_CU_WORD + __smid()] workgroups on that CU still on their own envs
 // (__smid() < 1024: XCC, SE, CU id bits); the block is zeroed per launch
 constexpr uint32_t GPOOL_CU_WORD = 16, GPOOL_CTL_BYTES = 4u * (GPOOL_CU_WORD + 1024u);
+// the pool is on by default for fused launches (several env steps) and for launches whose update cap is at least
+// this (pbn_abi.cpp env_launch): one env step at config 5's 4,096 cap lost more to the waiting workgroups'
+// residency than the moved envs gave back (1.14 -> 1.18-1.20 ms per step)
+constexpr uint32_t GPOOL_MIN_CAP = 16384;
 
 constexpr uint32_t MT_ROW = 624;
 
