@@ -179,6 +179,8 @@ struct pbn_batch {
     // and update caps from GPOOL_MIN_CAP (below it one env step's loops are too short to repay the waiting
     // workgroups' residency)
     int env_grid_steal = -1;
+    int env_migrate_blocks = -1;  // PBNSIM_ENV_MIGRATE_BLOCKS: k_env grid pool, lone tail sessions move after this many
+                                  // blocks (0 = never), -1 = GPOOL_MIGRATE_BLOCKS
     int env_grid_slots = 0;      // PBNSIM_ENV_GRID_SLOTS: pool slots in use (measurement: 1 keeps the waiting workgroups
                                  // resident but moves at most one env), 0 = GPOOL_CAP
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
@@ -544,6 +546,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = std::max(0, std::min(3, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_GRID_STEAL")) b->env_grid_steal = atoi(v) != 0 ? 1 : 0;
+    if (const char* v = getenv("PBNSIM_ENV_MIGRATE_BLOCKS")) b->env_migrate_blocks = std::max(0, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_GRID_SLOTS")) b->env_grid_slots = std::max(1, std::min((int)GPOOL_CAP, atoi(v)));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
@@ -1580,6 +1583,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
             a.gpool = reinterpret_cast<uint64_t*>(base + GPOOL_CTL_BYTES + st_bytes);
             a.gpool_cap = b->env_grid_slots > 0 ? (uint32_t)b->env_grid_slots : GPOOL_CAP;
             a.gpool_epoch = b->gpool_epoch;
+            a.gpool_migrate = b->env_migrate_blocks >= 0 ? (uint32_t)b->env_migrate_blocks : GPOOL_MIGRATE_BLOCKS;
             b->gpool_last = true;
         }
     }
@@ -1793,15 +1797,16 @@ int pbn_env_grid_stats(pbn_batch* b, uint32_t* stats) {
     CHECK_NN(b, "batch");
     CHECK_NN(stats, "stats");
     SET_DEV(b);
-    for (int k = 0; k < 4; k++) stats[k] = 0;
+    for (int k = 0; k < 5; k++) stats[k] = 0;
     if (!b->gpool_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
-    uint32_t ctl[5];
+    uint32_t ctl[6];
     HIP_TRY(hipMemcpy(ctl, b->s_gpool.p, sizeof ctl, hipMemcpyDeviceToHost));
     stats[0] = ctl[3];  // envs pushed
     stats[1] = ctl[1];  // tickets taken
     stats[2] = ctl[4];  // waits given up
     stats[3] = ctl[2];  // live count at the end (0 after a complete launch)
+    stats[4] = ctl[5];  // of the pushed envs, sessions moved mid-way
     return 0;
 }
 

@@ -1533,6 +1533,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 }
                 // ring mode (helpers recruited): ringH = the session's helpers (0: self-prepared blocks)
                 uint32_t ringH = 0;
+                bool migrated = false;  // the env went to the grid pool mid-session (lane L holds no env now)
                 uint32_t rblocks = 0, rwaits = 0;  // ring diagnostics (pbn_env_tail_stats)
                 uint32_t* const rcs = rctl_of(wv_in_wg);
                 TailDraw D = prepare(0u);
@@ -1643,11 +1644,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     // ring blocks (the self-prepared block k + 1 in D is dropped)
                     if (a.steal_local && (++nblk & 15u) == 0u && !fin) {
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
-                        if (others) {
-                            local_push(others);
-                            grid_push(__ballot(e >= 0) & ~(1ull << L));
+                        if (others) local_push(others);
+                        const bool alone = !(SPLIT && a.tail_helpers && ring_R >= 3u && ldl(&wctl[1]) != 0u);
+                        if (GRID && alone && a.tail_helpers && ring_R >= 3u && a.gpool_migrate && nblk >= a.gpool_migrate) {
+                            // a long session no idle sibling can help: the env itself moves to a CU that has run
+                            // out of work, whose idle waves become its helpers (0.41 vs 0.7-0.85 us per 64
+                            // updates); its words as the session has them (used, counters; the plane is committed)
+                            if (lane == L) {
+                                used = u;
+                                m_lo = m;
+                            }
+                            grid_push(1ull << L);
+                            if (__shfl((int)(e < 0), (int)L)) {
+                                migrated = true;
+                                if (lane == 0)
+                                    (void)__hip_atomic_fetch_add(gctl(5), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                return;
+                            }
                         }
-                        if (SPLIT && a.tail_helpers && ring_R >= 3u && ldl(&wctl[1]) != 0u) {
+                        if (others) grid_push(__ballot(e >= 0) & ~(1ull << L));
+                        if (!alone) {
                             const uint32_t cl = claim_idle(min((uint32_t)a.tail_helpers, 3u));
                             if (cl) {
                                 const uint32_t H = (uint32_t)__popc(cl);
@@ -1871,7 +1887,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     est[39] = sess_u0;
                 }
 #endif
-                if (lane == L) {
+                if (lane == L && !migrated) {
                     used = u;
                     m_lo = m;
                     capped = !hitf;

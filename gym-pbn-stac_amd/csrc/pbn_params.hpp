@@ -127,12 +127,15 @@ struct EnvArgs {
     // fast == 4 (with steal_local): grid-wide hand-off of tail envs to workgroups that have run out of work
     // (k_env, "grid pool"). Device memory, control words zeroed per launch:
     uint32_t* gpool_ctl;      // [0] slots reserved by pushers, [1] tickets taken by idle workgroups, [2] live:
-                              // workgroups working + envs in the pool, [3] envs pushed, [4] waits given up
+                              // workgroups working + envs in the pool, [3] envs pushed, [4] waits given up,
+                              // [5] of the pushed, sessions moved mid-way (a long session no sibling could help)
     uint32_t* gpool_state;    // [gpool_cap] per slot: epoch << 2 | 1 (a pusher claimed it) or | 2 (its ticket
                               // holder gave up on it); any other epoch: unclaimed
     uint64_t* gpool;          // [gpool_cap][GPOOL_GRANULES] 8-B {epoch, value} granules: one env's hand-off words
     uint32_t gpool_cap;       // slots; 0 = grid hand-off off
     uint32_t gpool_epoch;     // this launch's tag (1 .. 2^30 - 1, a new one per launch)
+    uint32_t gpool_migrate;   // a tail session that has run this many blocks with no idle sibling to help it moves
+                              // itself into the pool (0 = never; GPOOL_MIGRATE_BLOCKS by default)
 };
 
 constexpr uint32_t GPOOL_GRANULES = 64;  // per slot: the hand-off box as u32 words (10 + 4W <= 64 for W <= 13)
@@ -144,6 +147,9 @@ constexpr uint32_t GPOOL_CU_WORD = 16, GPOOL_CTL_BYTES = 4u * (GPOOL_CU_WORD + 1
 // this (pbn_abi.cpp env_launch): one env step at config 5's 4,096 cap lost more to the waiting workgroups'
 // residency than the moved envs gave back (1.14 -> 1.18-1.20 ms per step)
 constexpr uint32_t GPOOL_MIN_CAP = 16384;
+// sessions moved mid-way: 16 / 64 / 256 blocks / never measured within run-to-run noise of each other at config 5's
+// shard (profiles/r05_r6_grid_pool_ab.json "migrate_threshold"); 256 keeps it to the longest sessions
+constexpr uint32_t GPOOL_MIGRATE_BLOCKS = 256;
 
 constexpr uint32_t MT_ROW = 624;
 

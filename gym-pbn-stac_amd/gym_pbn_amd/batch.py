@@ -419,10 +419,10 @@ class PBNBatch:
 
     def env_grid_stats(self) -> dict:
         """The last R6 launch's grid-pool counters: envs handed to workgroups that had run out of work,
-        tickets those workgroups took, waits given up (0), live count at the end (0)."""
-        st = (C.c_uint32 * 4)()
+        tickets those workgroups took, waits given up (0), live count at the end (0), sessions moved mid-way."""
+        st = (C.c_uint32 * 5)()
         L.check(L.lib.pbn_env_grid_stats(self._h, st))
-        return {"pushed": st[0], "tickets": st[1], "gave_up": st[2], "live_at_end": st[3]}
+        return {"pushed": st[0], "tickets": st[1], "gave_up": st[2], "live_at_end": st[3], "migrated": st[4]}
 
     def env_handoffs(self) -> int:
         """Envs the last R6 launch handed from tail-mode waves to idle ones (0 with the hand-off off)."""

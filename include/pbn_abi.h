@@ -265,10 +265,11 @@ int pbn_env_tail_helpers(pbn_batch *b, uint32_t *count);
  * sessions read from their helpers' rings, and of those the blocks not yet written when the session reached
  * them (the session waited). Syncs the batch stream. Diagnostics. */
 int pbn_env_tail_stats(pbn_batch *b, uint32_t *stats);
-/* The last R6 launch's grid-pool counters, stats[4] (env_kernel 4 with the hand-off on; PBNSIM_ENV_GRID_STEAL=0
- * turns the pool off): envs a tail wave handed to a workgroup that had run out of work (anywhere on the GPU),
- * tickets those workgroups took, waits given up (0 unless a launch failed with PBN_E_HIP), and the live count
- * at the launch's end (0). Syncs the batch stream. Diagnostics. */
+/* The last R6 launch's grid-pool counters, stats[5] (env_kernel 4 with the hand-off on; on by default for fused
+ * launches and update caps >= 16,384, PBNSIM_ENV_GRID_STEAL=0/1 forces it): envs a tail wave handed to a workgroup
+ * that had run out of work (anywhere on the GPU), tickets those workgroups took, waits given up (0 unless a launch
+ * failed with PBN_E_HIP), the live count at the launch's end (0), and of the envs handed over, sessions moved
+ * mid-way (a long tail session no idle sibling could help). Syncs the batch stream. Diagnostics. */
 int pbn_env_grid_stats(pbn_batch *b, uint32_t *stats);
 
 #ifdef __cplusplus

@@ -345,7 +345,7 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
     b.close()
 
 
-@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off", "grid", "grid_off"])
+@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off", "grid", "grid_off", "migrate"])
 @pytest.mark.parametrize("mode", ["per_step", "fused"])
 def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypatch, mode, case):
     """A case in which the workgroup hand-off must happen: one workgroup (4 waves), two
@@ -365,16 +365,21 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     goes idle, so the other workgroup waits on a ticket while the loaded wave, after handing three envs
     to its idle siblings, still holds unstarted ones: it pushes envs into the pool (asserted) and the
     waiting workgroup resumes them; every output equals the oracle. ``grid_off``: PBNSIM_ENV_GRID_STEAL=0
-    (nothing pushed)."""
+    (nothing pushed). ``migrate``: the same two workgroups with 4 envs -- the loaded wave hands three to its
+    siblings, so all four waves of its workgroup run long sessions with no idle wave to help them, and at a
+    16-block check a session moves itself (mid-way: used, counters, committed plane) to the waiting
+    workgroup (asserted), which resolves the rest with helpers; exact against the oracle."""
     import torch
 
-    grid_case = case.startswith("grid")
+    grid_case = case.startswith("grid") or case == "migrate"
     monkeypatch.setenv("PBNSIM_ENV_LANES", "16" if grid_case else "2")
     monkeypatch.setenv("PBNSIM_ENV_GRID", "2" if grid_case else "1")
     if case == "helpers_off":
         monkeypatch.setenv("PBNSIM_ENV_HELPERS", "0")
     if case == "grid_off":
         monkeypatch.setenv("PBNSIM_ENV_GRID_STEAL", "0")
+    if case == "migrate":
+        monkeypatch.setenv("PBNSIM_ENV_MIGRATE_BLOCKS", "16")  # at the first 16-block check (default: 256)
     import sys
     from pathlib import Path
 
@@ -388,7 +393,8 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
                 horizon=100)
     o = oracle_mod.Oracle(net)
-    B, seed, base, T, A, cap = (6 if case == "handoff" else 16 if grid_case else 2), 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
+    B = {"handoff": 6, "grid": 16, "grid_off": 16, "migrate": 4}.get(case, 2)
+    seed, base, T, A, cap = 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     # per env, the first candidate action row (oracle) whose first env step runs >= 2,048 updates
@@ -440,6 +446,8 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     assert all(p["gave_up"] == 0 and p["live_at_end"] == 0 for p in pool), pool
     if case == "grid":
         assert pool[0]["pushed"] > 0, pool  # ... and push envs to the waiting workgroup
+    if case == "migrate":
+        assert pool[0]["migrated"] > 0, pool  # ... and move a running session there
     if case == "grid_off":
         assert sum(p["pushed"] + p["tickets"] for p in pool) == 0, pool
     if case == "helpers":

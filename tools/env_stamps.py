@@ -111,6 +111,17 @@ def main():
         lt = st[:, 35] > 0  # the wave's last tail block's end (realtime)
         res["last_tail_block_end_us"] = pct((st[lt, 35] - t0) / 100.0) if lt.any() else None
         res["envs_from_grid_pool"] = int((st[:, 16] >> 16).sum())
+        # the critical path: the waves whose last tail block ends last, and their longest session
+        order = np.argsort(-st[:, 35])[:5]
+        res["last_waves"] = [{"last_block_end_us": round(float((st[w, 35] - t0) / 100.0), 1),
+                              "lane_phase_le16_us": round(float((st[w, 4] - t0) / 100.0), 1) if st[w, 4] else None,
+                              "longest_session_start_us": round(float((st[w, 36] - t0) / 100.0), 1) if st[w, 36] else None,
+                              "longest_session_blocks": int(st[w, 37]),
+                              "longest_session_end_us": round(float((st[w, 38] - t0) / 100.0), 1) if st[w, 38] else None,
+                              "updates_before_session": int(st[w, 39]),
+                              "tail_blocks": int(st[w, 19]), "envs_received": int(st[w, 15]),
+                              "from_pool": int(st[w, 16] >> 16), "pushed_local": int(st[w, 16] & 0xFFFF)}
+                             for w in order]
         res["tail_blocks"] = int(st[:, 19].sum())
         res["tail_block_us_mean"] = round(float(st[:, 32].sum() / max(st[:, 19].sum(), 1) / 100.0), 4)
         res["tail_block_rounds_mean"] = round(float(st[:, 21].sum() / max(st[:, 19].sum(), 1)), 3)
