@@ -179,6 +179,8 @@ struct pbn_batch {
     // and update caps from GPOOL_MIN_CAP (below it one env step's loops are too short to repay the waiting
     // workgroups' residency)
     int env_grid_steal = -1;
+    int env_pool_cu_idle = -1;    // PBNSIM_ENV_POOL_CU_IDLE: 1 only idle CUs take pool tickets, 0 any idle workgroup,
+                                  // -1 = the default (1)
     int env_migrate_blocks = -1;  // PBNSIM_ENV_MIGRATE_BLOCKS: k_env grid pool, lone tail sessions move after this many
                                   // blocks (0 = never), -1 = GPOOL_MIGRATE_BLOCKS
     int env_grid_slots = 0;      // PBNSIM_ENV_GRID_SLOTS: pool slots in use (measurement: 1 keeps the waiting workgroups
@@ -546,6 +548,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = std::max(0, std::min(3, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_GRID_STEAL")) b->env_grid_steal = atoi(v) != 0 ? 1 : 0;
+    if (const char* v = getenv("PBNSIM_ENV_POOL_CU_IDLE")) b->env_pool_cu_idle = atoi(v) != 0 ? 1 : 0;
     if (const char* v = getenv("PBNSIM_ENV_MIGRATE_BLOCKS")) b->env_migrate_blocks = std::max(0, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_GRID_SLOTS")) b->env_grid_slots = std::max(1, std::min((int)GPOOL_CAP, atoi(v)));
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
@@ -1583,6 +1586,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
             a.gpool = reinterpret_cast<uint64_t*>(base + GPOOL_CTL_BYTES + st_bytes);
             a.gpool_cap = b->env_grid_slots > 0 ? (uint32_t)b->env_grid_slots : GPOOL_CAP;
             a.gpool_epoch = b->gpool_epoch;
+            a.gpool_cu_idle = b->env_pool_cu_idle != 0 ? 1u : 0u;
             a.gpool_migrate = b->env_migrate_blocks >= 0 ? (uint32_t)b->env_migrate_blocks : GPOOL_MIGRATE_BLOCKS;
             b->gpool_last = true;
         }

@@ -134,6 +134,8 @@ struct EnvArgs {
     uint64_t* gpool;          // [gpool_cap][GPOOL_GRANULES] 8-B {epoch, value} granules: one env's hand-off words
     uint32_t gpool_cap;       // slots; 0 = grid hand-off off
     uint32_t gpool_epoch;     // this launch's tag (1 .. 2^30 - 1, a new one per launch)
+    uint32_t gpool_cu_idle;   // 1: a workgroup takes tickets only once no workgroup of its CU is on its own envs;
+                              // 0: as soon as its own waves have run out of work
     uint32_t gpool_migrate;   // a tail session that has run this many blocks with no idle sibling to help it moves
                               // itself into the pool (0 = never; GPOOL_MIGRATE_BLOCKS by default)
 };
