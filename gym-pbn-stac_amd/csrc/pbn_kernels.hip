@@ -760,9 +760,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     // buffer, counts the claimed wave busy and raises its flag; the claimed wave resumes the env in
     // lane 0. Bit-exact: the env's Philox stream is keyed by its global id, update index and env step,
     // not by the wave. A wave leaves when no wave of its workgroup is busy and it can clear its own
-    // idle bit (nobody claimed it). Tried and dropped: the same between any waves of the grid through
-    // device-memory slots -- correct, but 7-20x slower (every cross-XCD read has to be an atomic, and
-    // pushers stalled for milliseconds behind them).
+    // idle bit (nobody claimed it). Between workgroups: the grid pool below (round 3's per-wave device
+    // mailboxes, where every cross-XCD read was an atomic, measured 7-20x slower).
     const uint32_t wv_in_wg = threadIdx.x >> 6;
     auto box_of = [&](uint32_t w) {
         return reinterpret_cast<uint64_t*>(lds + a.off_gen + w * GWB + CH * 128 + 64);
