@@ -125,6 +125,8 @@ def main():
         res["tail_blocks"] = int(st[:, 19].sum())
         res["tail_block_us_mean"] = round(float(st[:, 32].sum() / max(st[:, 19].sum(), 1) / 100.0), 4)
         res["tail_block_rounds_mean"] = round(float(st[:, 21].sum() / max(st[:, 19].sum(), 1)), 3)
+        # shader clock while in tail blocks: s_memtime cycles (est 20) per s_memrealtime 10-ns tick (est 32)
+        res["tail_clock_GHz"] = round(float(st[:, 20].sum() / max(st[:, 32].sum(), 1) / 10.0), 4)
         res["chunks_per_wave_p50"] = float(np.median(st[:, 8]))
         res["mean_active_lanes_per_chunk_p50"] = float(np.median(st[:, 9] / np.maximum(st[:, 8], 1)))
         out["reps"].append(res)
