@@ -1392,7 +1392,7 @@ static std::vector<uint8_t> env_gen_image(const pbn_envcfg* cfg, uint32_t erec_s
             memcpy(g.data() + 4 * ((size_t)i * tp4 + q), &v, 4);
         }
     memcpy(g.data() + cfg->off_cubes + erec_shift, im + cfg->off_cubes, L.bytes - cfg->off_cubes);
-    const uint32_t nd_off = cfg->off_ndelta + erec_shift, ROW = BLOCK * 4u;
+    const uint32_t nd_off = cfg->off_ndelta + erec_shift, ROW = ENV_BLOCK * 4u;
     auto off = [&](uint32_t x) { return (x >> 5) * ROW; };
     for (uint32_t i = 0; i < N; i++)
         for (uint32_t q = 0; q < rs; q++) {
@@ -1442,7 +1442,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         const uint32_t nrec = (uint32_t)b->net->N * std::max(tp4 + 1u, cfg->L.pmax);
         erec_shift = cfg->L.off_rec + 16u * nrec - cfg->off_cubes;
         erec_fits = nrec <= 65535u &&
-                    env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1, 0, ENV_CHUNK_SMALL) <= 64u * 1024u;
+                    env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 2, 1, 0, ENV_CHUNK_SMALL) <= ENV_LDS_MAX;
     }
     // group mode (k_env_grp: G lanes per env, G updates per round trip; its rows need no env records)
     int grp = 1;
@@ -1457,7 +1457,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         else if (cfg->H <= 4)
             mode = 4;  // the same kernel with one packed counter word (<= 4 cubes)
         // mode 4 adds the workgroup hand-off control words: re-check the fit with the final mode
-        if (mode == 4 && env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 4, 1, 0, ENV_CHUNK_SMALL) > 64u * 1024u)
+        if (mode == 4 && env_lds_bytes(b->W, cfg->L.bytes + erec_shift, 4, 1, 0, ENV_CHUNK_SMALL) > ENV_LDS_MAX)
             mode = cfg->fast;
     }
     if (mode != 2 && mode != 4) erec_shift = 0;
@@ -1484,11 +1484,11 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
         const uint32_t img = cfg->L.bytes + erec_shift;
         if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, img, &bpc_s, b->net->N, ENV_CHUNK_SMALL))
             return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
-        const bool large_fits = env_lds_bytes(b->W, img, mode, 1, 0, ENV_CHUNK_LARGE) <= 64u * 1024u;
+        const bool large_fits = env_lds_bytes(b->W, img, mode, 1, 0, ENV_CHUNK_LARGE) <= ENV_LDS_MAX;
         if (large_fits)
             if (int e = max_blocks_env(b->W, b->net->kind, mode, grp, img, &bpc_l, b->net->N, ENV_CHUNK_LARGE))
                 return fail(PBN_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)e));
-        const uint64_t lanes_l = (uint64_t)b->n_cu * (uint64_t)bpc_l * BLOCK;
+        const uint64_t lanes_l = (uint64_t)b->n_cu * (uint64_t)bpc_l * ENV_BLOCK;
         const bool throughput = n_calls >= 16u && b->B >= 4u * lanes_l && bpc_s > bpc_l;
         chunk = large_fits && !throughput ? ENV_CHUNK_LARGE : ENV_CHUNK_SMALL;
         if (b->env_chunk == (int)ENV_CHUNK_SMALL || (b->env_chunk == (int)ENV_CHUNK_LARGE && large_fits))
@@ -1520,7 +1520,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     // queue when it is done (PBNSIM_ENV_LANES overrides; 64 = lane mode, the tail at the end)
     a.lane_limit = 64u;
     if (mode == 4) {
-        const uint64_t slots = (uint64_t)b->n_cu * (uint64_t)bpc * (BLOCK / 64);
+        const uint64_t slots = (uint64_t)b->n_cu * (uint64_t)bpc * (ENV_BLOCK / 64);
         if (b->env_lane_limit > 0)
             a.lane_limit = (uint32_t)b->env_lane_limit;
         else if (a.tail_max >= 1 && b->B <= ENV_ONE_LANE_ENVS_PER_SLOT * slots)
@@ -1529,7 +1529,7 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     a.fast = mode;
     a.grp = grp;
     a.chunk = chunk;
-    a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + erec_shift + 8u * (uint32_t)b->W * BLOCK;
+    a.off_gen = mode == 3 ? cfg->L.bytes : cfg->L.bytes + erec_shift + 8u * (uint32_t)b->W * ENV_BLOCK;
     if (int rc = b->s_counter.ensure(8)) return rc;
     a.counter = (unsigned long long*)b->s_counter.p;
     a.n_cubes = cfg->H;
@@ -1552,7 +1552,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
     HIP_TRY(hipMemsetAsync(b->d_error, 0, 4, b->stream));
     HIP_TRY(hipMemsetAsync(b->s_counter.p, 0, 8, b->stream));
     // lanes per env (group mode) or, with a lane limit, 64 / limit lane slots per env
-    int grid = b->grid_for(a.lane_limit < 64u ? (b->B * 64u + a.lane_limit - 1u) / a.lane_limit : b->B * (uint64_t)grp, bpc);
+    int grid = b->grid_for(a.lane_limit < 64u ? (b->B * 64u + a.lane_limit - 1u) / a.lane_limit : b->B * (uint64_t)grp, bpc,
+                           env_block(mode));
     // PBNSIM_ENV_GRID: exactly that many workgroups (at most the resident count; persistent waves: any grid
     // drains the counter, and surplus workgroups find the queue empty)
     if (b->env_grid_cap) grid = std::min(b->env_grid_cap, b->n_cu * bpc);

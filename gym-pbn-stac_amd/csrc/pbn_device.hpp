@@ -322,7 +322,7 @@ __device__ __forceinline__ uint32_t table_eval_lds(const P_t& P, uint32_t i, uin
 }
 
 // Env record (k_env, cooperative-draw mode): predictor record rec (in0 | in1<<16 | in2<<32 | tt<<48)
-// of node i re-encoded for the LDS state planes of 256-lane workgroups: byte offsets of the plane
+// of node i re-encoded for the LDS state planes of k_env's workgroups (ENV_BLOCK lanes): byte offsets of the plane
 // dwords holding in0 / in1 (x), in2 / node i (y), tt | i << 16
 // (w): the bit positions of in0, in1, in2, i in those dwords (one byte each). An update then reads
 // its four plane dwords with no index arithmetic. Inputs are < 512 (W <= 8), so every offset is
@@ -332,7 +332,7 @@ __device__ __forceinline__ uint32_t table_eval_lds(const P_t& P, uint32_t i, uin
 __device__ __forceinline__ uint4 env_record(uint64_t rec, uint32_t i, uint32_t nd_off) {
     const uint32_t x0 = (uint32_t)rec & 0xFFFFu, x1 = (uint32_t)(rec >> 16) & 0xFFFFu,
                    x2 = (uint32_t)(rec >> 32) & 0xFFFFu;
-    auto off = [](uint32_t x) { return (x >> 5) * (uint32_t)(BLOCK * 4); };
+    auto off = [](uint32_t x) { return (x >> 5) * (uint32_t)(ENV_BLOCK * 4); };
     return make_uint4(off(x0) | (off(x1) << 16), off(x2) | (off(i) << 16),
                       (x0 & 31u) | ((x1 & 31u) << 8) | ((x2 & 31u) << 16) | ((i & 31u) << 24),
                       (uint32_t)(rec >> 48) | ((nd_off + 8u * i) << 16));

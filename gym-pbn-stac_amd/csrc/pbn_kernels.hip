@@ -642,7 +642,7 @@ static_assert(ENV_CHUNK_SMALL % 8u == 0 && ENV_CHUNK_LARGE % 8u == 0 && ENV_UNRO
               "draw-round chunks: multiples of the unroll (and of 4: the own-draw iteration)");
 
 template <int W, int KIND, int REPLAY, int FAST>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_env(EnvArgs a) {
+__global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_env(EnvArgs a) {
     constexpr bool GEN = FAST == 2 || FAST == 4;
     constexpr bool ONE_WORD = FAST == 4;  // <= 4 cubes: the high counter word is never read
     constexpr bool TAIL = FAST == 4;      // wave-wide tail mode (see below)
@@ -669,17 +669,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         // compact image (the env config's image does not carry it)
         const uint64_t* gthr = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(a.img) + a.L.off_thr);
         const uint32_t tp = a.L.tp, tp4 = X.tp4, rs = X.rs;
-        for (uint32_t k = threadIdx.x; k < N * tp4; k += BLOCK) {
+        for (uint32_t k = threadIdx.x; k < N * tp4; k += ENV_BLOCK) {
             const uint32_t i = k / tp4, q = k - i * tp4;
             const uint64_t t = q < tp ? u32_threshold(gthr[i * tp + q]) : (1ull << 32);
             reinterpret_cast<uint32_t*>(lds)[k] = t >> 32 ? 0xFFFFFFFFu : (uint32_t)t;
         }
         const uint32_t tail = a.off_cubes - a.erec_shift;  // the cubes' offset in the device image
-        for (uint32_t k = threadIdx.x; k < (a.L.bytes - tail) / 16; k += BLOCK)
+        for (uint32_t k = threadIdx.x; k < (a.L.bytes - tail) / 16; k += ENV_BLOCK)
             l[(tail + a.erec_shift) / 16 + k] = g[tail / 16 + k];
         const uint64_t* grec = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(a.img) + a.L.off_rec);
         uint4* erec = reinterpret_cast<uint4*>(lds + a.L.off_rec);
-        for (uint32_t r = threadIdx.x; r < N * rs; r += BLOCK) {
+        for (uint32_t r = threadIdx.x; r < N * rs; r += ENV_BLOCK) {
             const uint32_t i = r / rs, q = r - i * rs;
             uint32_t src = q;
             if (q == tp4) {  // the node's thresholds below 2^32 on a (a prefix: non-decreasing)
@@ -696,12 +696,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     // the launch's draw-round chunk (GEN) and the per-wave draw buffer it sizes
     const uint32_t CH = GEN ? a.chunk : ENV_CHUNK;
     const uint32_t GWB = env_gen_wave_bytes(CH);
-    uint32_t* const wctl = reinterpret_cast<uint32_t*>(lds + a.off_gen + (BLOCK / 64) * GWB);
+    uint32_t* const wctl = reinterpret_cast<uint32_t*>(lds + a.off_gen + (ENV_BLOCK / 64) * GWB);
     // grid pool words: device memory, every access a global agent-scope atomic (sc1: past the CU's L1)
     auto gctl = [&](int k) { return (gu32*)(a.gpool_ctl + k); };
     const bool GRID = TAIL && a.steal_local && a.gpool_cap != 0u;
     if (TAIL && a.steal_local && threadIdx.x == 0) {
-        wctl[0] = BLOCK / 64;  // busy
+        wctl[0] = ENV_BLOCK / 64;  // busy
         wctl[1] = 0u;          // idle mask
         wctl[2] = 0u;          // grid pool: a wave of this workgroup is waiting on a ticket
         wctl[3] = 0u;          // grid pool: 1 the launch's work is done, leave; 2 this workgroup left its CU's count
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         }
     }
     __syncthreads();
-    const PlaneT<BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes + a.erec_shift) + threadIdx.x};
+    const PlaneT<ENV_BLOCK> P{reinterpret_cast<uint32_t*>(lds + a.L.bytes + a.erec_shift) + threadIdx.x};
 #ifdef PBN_STAMPS
     // 0 start, 1 first chunk below ENV_OWN_DRAWS_MIN active lanes, 2 first chunk after a lane of the
     // wave found the work queue empty,
@@ -1356,7 +1356,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 };
                 auto erec_of = [&](uint32_t E) { return erec[E & 0xFFFFu]; };
                 // Writer round of a block (its records q): node n's 64-bit writer mask at wmc + 8n, n = plane
-                // offset / 32 | bit (offset = dword * 1024); or, read the four operands' masks, clear.
+                // offset / 32 | bit (offset = dword * 4 ENV_BLOCK); or, read the four operands' masks, clear.
                 struct WRound {
                     uint32_t nd;
                     uint64_t w0, w1, w2, wi;
@@ -1365,7 +1365,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                     WRound R;
                     R.nd = *reinterpret_cast<const uint32_t*>(lds + (q.w >> 16));
                     auto wadr = [&](uint32_t off, uint32_t bit) {
-                        return reinterpret_cast<unsigned long long*>(wmc + (off >> 2) + (bit << 3));
+                        return reinterpret_cast<unsigned long long*>(wmc + (off >> ENV_ROW_SHIFT) + (bit << 3));
                     };
                     const uint32_t z = q.z;
                     unsigned long long* const wi_p = wadr(q.y >> 16, z >> 24);
@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                             reinterpret_cast<uint4*>(wmc)[q2] = make_uint4(0u, 0u, 0u, 0u);
                         wave_sync();
                         auto nadr = [&](uint32_t off, uint32_t bit) {  // node entry {even, odd}
-                            return reinterpret_cast<unsigned long long*>(wmc + ((off >> 2) + (bit << 3)) * 2u);
+                            return reinterpret_cast<unsigned long long*>(wmc + ((off >> ENV_ROW_SHIFT) + (bit << 3)) * 2u);
                         };
                         const uint64_t bl = (1ull << lane) - 1ull, ul = (2ull << lane) - 1ull;
                         // code of the last earlier writer (t' = 2 l' + h', 7 bits) and whether there is one
@@ -2223,7 +2223,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     for (uint32_t k = 0; k < 64; ++k) est[14] += (uint32_t)__shfl((int)ncapped, (int)k);
     est[12] = blockIdx.x;
     est[13] = __smid();
-    const uint32_t wv = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    const uint32_t wv = blockIdx.x * (ENV_BLOCK / 64) + threadIdx.x / 64;
     if (lane == 0 && wv < 16384)
         for (int k = 0; k < ENV_STAMPS; ++k) g_env_stamps[(uint64_t)wv * ENV_STAMPS + k] = est[k];
 #endif
@@ -2756,11 +2756,11 @@ static void* flip_fn(int W) {
     return nullptr;
 }
 
-static int launch(void* fn, int grid, uint32_t lds, void* stream, void* args, size_t args_size) {
+static int launch(void* fn, int grid, uint32_t lds, void* stream, void* args, size_t args_size, int block = BLOCK) {
     if (!fn) return (int)hipErrorInvalidValue;
     (void)args_size;
     void* kargs[] = {args};
-    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, lds, (hipStream_t)stream);
+    return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3((unsigned)block), kargs, lds, (hipStream_t)stream);
 }
 
 uint32_t step_lds_bytes(int W, uint32_t image_bytes, int sb, int grp) {
@@ -2860,7 +2860,7 @@ int launch_env_multi(int W, const EnvArgs& a, int replay, int grid, void* stream
     EnvArgs c = a;
     return launch(fn, grid, env_lds_bytes(W, a.L.bytes + a.erec_shift, replay ? std::min(a.fast, 1) : a.fast, a.grp,
                                           a.L.n_nodes, a.chunk),
-                  stream, &c, sizeof c);
+                  stream, &c, sizeof c, env_block(a.fast));
 }
 
 static int occupancy(void* fn, int block, uint32_t lds, int* blocks_per_cu) {
@@ -2884,16 +2884,16 @@ int max_blocks_step(int W, int kind, uint32_t lds_bytes, int sb, int* blocks_per
 
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes, uint32_t chunk) {
     if (fast == 3) return image_bytes + 8u * (uint32_t)W * (BLOCK / (uint32_t)grp);  // one row per group
-    const uint32_t planes = image_bytes + 8u * (uint32_t)W * BLOCK;
+    const uint32_t planes = image_bytes + 8u * (uint32_t)W * ENV_BLOCK;
     (void)n_nodes;
     // fast == 4: 16 B of workgroup hand-off control after the per-wave draw buffers
-    return fast == 2 || fast == 4 ? planes + (BLOCK / 64) * env_gen_wave_bytes(chunk) + (fast == 4 ? 16u : 0u) : planes;
+    return fast == 2 || fast == 4 ? planes + (ENV_BLOCK / 64) * env_gen_wave_bytes(chunk) + (fast == 4 ? 16u : 0u) : planes;
 }
 
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes, uint32_t chunk) {
     void* fn = kind == KIND_PREDICTOR_MIX ? env_fn_w<KIND_PREDICTOR_MIX>(W, 0, fast, grp)
                                           : env_fn_w<KIND_PROB_TABLE>(W, 0, fast, grp);
-    return occupancy(fn, BLOCK, env_lds_bytes(W, lds_bytes, fast, grp, n_nodes, chunk), blocks_per_cu);
+    return occupancy(fn, env_block(fast), env_lds_bytes(W, lds_bytes, fast, grp, n_nodes, chunk), blocks_per_cu);
 }
 
 }  // namespace pbn

@@ -18,6 +18,17 @@ enum {
 enum { STORE_FULL = 0, STORE_DIRTY = 1 };
 
 constexpr int BLOCK = 256;          // 4 wave64 per workgroup
+#ifndef PBN_ENV_BLOCK
+#define PBN_ENV_BLOCK 256
+#endif
+// k_env's workgroup (lane / tail / hand-off modes; group mode k_env_grp keeps BLOCK): the workgroup is the
+// tail hand-off's and the helpers' domain
+constexpr int ENV_BLOCK = PBN_ENV_BLOCK;
+static_assert(ENV_BLOCK % 64 == 0 && ENV_BLOCK / 64 <= 16, "k_env: whole waves, idle mask / helper codes fit");
+// k_env's LDS budget per workgroup: 64 KiB at 256 threads (two workgroups per CU), the CU's 160 KiB above
+constexpr uint32_t ENV_LDS_MAX = ENV_BLOCK > 256 ? 160u * 1024u : 64u * 1024u;
+// a plane byte offset (dword * 4 * ENV_BLOCK) >> ENV_ROW_SHIFT = dword * 256: the tail writer-mask tables' row
+constexpr uint32_t ENV_ROW_SHIFT = __builtin_ctz((unsigned)ENV_BLOCK / 64u);
 constexpr int MAX_WORDS = 8;        // N <= 512
 constexpr uint32_t MAX_IMAGE = 48 * 1024;  // LDS bytes for the network image (state planes come on top)
 
@@ -256,6 +267,7 @@ constexpr uint32_t env_gen_wave_bytes(uint32_t chunk) { return chunk * 64u * 2u 
 int max_blocks_env(int W, int kind, int fast, int grp, uint32_t lds_bytes, int* blocks_per_cu, int n_nodes = 0,
                    uint32_t chunk = ENV_CHUNK_LARGE);
 uint32_t env_lds_bytes(int W, uint32_t image_bytes, int fast, int grp, int n_nodes = 0, uint32_t chunk = ENV_CHUNK_LARGE);
+inline int env_block(int fast) { return fast == 3 ? BLOCK : ENV_BLOCK; }  // threads per workgroup of the R6 kernel
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream);
 int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream);  // grid from the kernel's occupancy
 uint32_t ssd_block(const SSDArgs& a);

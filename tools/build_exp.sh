@@ -24,7 +24,7 @@ done
 cd $out/src
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -mcode-object-version=5 -Wno-pass-failed -I$out/include ${flags[*]}"
 for k in pbn_kernels pbn_mt pbn_ssd pbn_sync; do /opt/rocm/bin/hipcc $F -c -o $out/$k.o csrc/$k.hip & done
-g++ -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I$out/include -c -o $out/pbn_abi.o csrc/pbn_abi.cpp
+g++ -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I$out/include ${flags[*]} -c -o $out/pbn_abi.o csrc/pbn_abi.cpp
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libpbnsim.so $out/*.o -L/opt/rocm/lib -lamdhip64
 echo built $out/libpbnsim.so
