@@ -596,7 +596,10 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 #ifndef PBN_GPOOL_CHECK_TICKS
 #define PBN_GPOOL_CHECK_TICKS 500  // a tail wave looks for waiting workgroups at most every 5 us (100 MHz ticks)
 #endif
-constexpr uint64_t GPOOL_TIMEOUT_TICKS = 200000000ull;  // 2 s: a ticket holder gives up (error flag 2; never expected)
+constexpr uint64_t GPOOL_TIMEOUT_TICKS = 200000000ull;  // 2 s: a claimed slot's words never came (error flag 2; never expected)
+// a workgroup waiting on the pool this long (20 ms) without an env leaves quietly (its slot given up first), so a
+// long launch does not keep idle workgroups resident (measured 3-4 % on the others) or wait on them
+constexpr uint64_t GPOOL_GIVE_UP_TICKS = 2000000ull;
 
 // ceil(2^32 / n) for n = 2..63 (0 for n < 2): k / n == umulhi(k, kRankMagic[n]) for k < 2^16
 struct RankMagic {
@@ -941,9 +944,11 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                 __hip_atomic_store(&wctl[3], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 (void)__hip_atomic_fetch_add(cu, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            const uint64_t ta = __builtin_amdgcn_s_memrealtime();
             while (a.gpool_cu_idle && __hip_atomic_load(cu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-                if (__hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-                    leave = 1;
+                if (__hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
+                    __builtin_amdgcn_s_memrealtime() - ta > GPOOL_GIVE_UP_TICKS) {
+                    leave = 1;  // (no ticket taken yet: nothing to give up)
                     break;
                 }
                 __builtin_amdgcn_s_sleep(PBN_GPOOL_SLEEP);
@@ -955,6 +960,7 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
         const bool has_slot = ticket < a.gpool_cap;
         gu64* g = (gu64*)(a.gpool + (uint64_t)(has_slot ? ticket : 0u) * GPOOL_GRANULES);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool claimed = false;  // the quiet give-up found the slot claimed: its words are on their way
         for (uint32_t it = 0;; ++it) {
             // lane 0 polls the slot's last granule; once it carries the epoch, the whole wave sweeps the slot
             int seen = 0;
@@ -975,12 +981,22 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
             if ((it & 1u) == 1u) {
                 int leave = 0;
                 if (lane == 0) {
-                    if (__hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                    if (!claimed && __hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
                         // nothing live: no push can come any more -- unless one already claimed this slot
                         leave = !has_slot || (__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u,
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE;
+                        claimed = !leave;
                     }
-                    if (!leave && __builtin_amdgcn_s_memrealtime() - t0 > GPOOL_TIMEOUT_TICKS) {
+                    const uint64_t waited = __builtin_amdgcn_s_memrealtime() - t0;
+                    if (!leave && !claimed && waited > GPOOL_GIVE_UP_TICKS) {
+                        // waited long with no env: give the slot up (as above) and leave, unless a push claimed it
+                        if (!has_slot || (__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE)
+                            leave = 1;
+                        else
+                            claimed = true;
+                    }
+                    if (!leave && claimed && waited > GPOOL_TIMEOUT_TICKS) {
                         leave = 1;
                         (void)__hip_atomic_fetch_add(gctl(4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         atomicOr(a.error, 2);
