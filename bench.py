@@ -177,6 +177,14 @@ def read_pmc(path: str, key: str):
     return pmc.get("per_launch_bytes", {}).get(key), pmc.get("source")
 
 
+def read_pmc_window(path: str, key: str):
+    """The launch window [lo, hi) the committed PMC median was taken over (tools/pmc_traffic.py), or None."""
+    try:
+        return json.loads(Path(path).read_text()).get("detail", {}).get(key, {}).get("window")
+    except (OSError, ValueError):
+        return None
+
+
 class MemFloor:
     """tools/libmallprobe.so: the step kernel's memory pattern without compute (see mall_probe.hip)."""
 
@@ -271,6 +279,9 @@ def beyond_mall_supplement(net, device, seed, floor):
     if traffic:
         out["traffic_GBs"] = traffic / s / 1e9
         out["traffic_frac"] = traffic / s / 1e9 / HBM_PEAK_GBS
+        out["traffic_over_alg"] = traffic / alg
+        out["traffic_window"] = read_pmc_window(str(ROOT / "profiles" / "pmc_traffic.json"), f"{net.name}:{B}")
+        out["timed_window"] = [W_, W_ + K_]
     if floor is not None:
         fl = floor.us_per_launch(B, round(100 * q), 50)
         out["floor_us"] = fl
@@ -863,12 +874,16 @@ def main():
                         "envs whose bit changed, so this is accounting, not moved bytes"},
             "traffic_source": pmc_src,
             "traffic_GBs": (traffic / avg_kernel_s / 1e9) if (traffic and launches) else None,
+            "traffic_over_alg": (traffic / alg_bytes) if traffic else None,
+            "traffic_window": read_pmc_window(args.pmc_file, f"{args.network}:{B}"),
+            "timed_window": [args.warmup, args.warmup + args.steps],
         }
         bm = sup.get("beyond_mall_8m")
         if bm and "error" not in bm:
             rf["hbm_8m"] = {k: bm.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
                                                    "traffic_frac", "avg_kernel_us", "changed_env_frac",
-                                                   "alg_bytes_per_launch", "floor_us", "frac_of_floor")}
+                                                   "alg_bytes_per_launch", "floor_us", "frac_of_floor",
+                                                   "traffic_over_alg", "traffic_window", "timed_window")}
         if isinstance(copy, float):
             rf["achievable_copy_GBs"] = copy
             rf["achievable_copy_source"] = "torch device-to-device copy of 2 GiB (past the MALL), read + write bytes"

@@ -159,6 +159,7 @@ struct pbn_batch {
     uint64_t* d_state = nullptr;
     int64_t* d_nsteps = nullptr;
     int32_t* d_error = nullptr;
+    bool fault_check = false;  // a device-path env launch used the grid pool since the last pbn_sync
     const void* d_image = nullptr;
     int n_cu = 0, bpc_step = 1, bpc_env = 1, bpc_base = 1, bpc_roll = 1;
     int step_block = 1024;  // threads per workgroup of the Philox step kernel (256 or 1024)
@@ -181,8 +182,6 @@ struct pbn_batch {
     int env_grid_steal = -1;
     int env_pool_cu_idle = -1;    // PBNSIM_ENV_POOL_CU_IDLE: 1 only idle CUs take pool tickets, 0 any idle workgroup,
                                   // -1 = the default (1)
-    int env_migrate_blocks = -1;  // PBNSIM_ENV_MIGRATE_BLOCKS: k_env grid pool, lone tail sessions move after this many
-                                  // blocks (0 = never), -1 = GPOOL_MIGRATE_BLOCKS
     int env_grid_slots = 0;      // PBNSIM_ENV_GRID_SLOTS: pool slots in use (measurement: 1 keeps the waiting workgroups
                                  // resident but moves at most one env), 0 = GPOOL_CAP
     int ssd_wave = -1;        // PBNSIM_SSD_WAVE: 1 = one wave per env, 0 = one lane per env, -1 = by size
@@ -548,9 +547,10 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     if (const char* v = getenv("PBNSIM_ENV_KERNEL_IMAGE")) b->env_kernel_image = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_ENV_HELPERS")) b->env_helpers = std::max(0, std::min(3, atoi(v)));
     if (const char* v = getenv("PBNSIM_ENV_GRID_STEAL")) b->env_grid_steal = atoi(v) != 0 ? 1 : 0;
+#ifdef PBN_MEASURE_KNOBS  // A/B-only knobs: tools/build_exp.sh -DPBN_MEASURE_KNOBS
     if (const char* v = getenv("PBNSIM_ENV_POOL_CU_IDLE")) b->env_pool_cu_idle = atoi(v) != 0 ? 1 : 0;
-    if (const char* v = getenv("PBNSIM_ENV_MIGRATE_BLOCKS")) b->env_migrate_blocks = std::max(0, atoi(v));
     if (const char* v = getenv("PBNSIM_ENV_GRID_SLOTS")) b->env_grid_slots = std::max(1, std::min((int)GPOOL_CAP, atoi(v)));
+#endif
     if (const char* v = getenv("PBNSIM_SSD_WAVE")) b->ssd_wave = atoi(v) ? 1 : 0;
     if (const char* v = getenv("PBNSIM_SSD_SERIAL")) b->ssd_serial = atoi(v) != 0;
     if (const char* v = getenv("PBNSIM_SSD_SHARED")) {
@@ -571,8 +571,10 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     size_t sb = 8 * (size_t)b->W * n_envs;
     if (hipMalloc(&b->d_state, sb) != hipSuccess) return bail(fail(PBN_E_NOMEM, "state alloc (%zu B)", sb));
     if (hipMalloc(&b->d_nsteps, 8 * n_envs) != hipSuccess) return bail(fail(PBN_E_NOMEM, "n_steps alloc"));
-    if (hipMalloc(&b->d_error, 4) != hipSuccess) return bail(fail(PBN_E_NOMEM, "error flag alloc"));
-    if (hipMemsetAsync(b->d_state, 0, sb, b->stream) != hipSuccess ||
+    // [0] the launch's error flags (zeroed per launch), [1] sticky grid-pool faults of device-path env
+    // launches, read and cleared by pbn_sync
+    if (hipMalloc(&b->d_error, 8) != hipSuccess) return bail(fail(PBN_E_NOMEM, "error flag alloc"));
+    if (hipMemsetAsync(b->d_error, 0, 8, b->stream) != hipSuccess || hipMemsetAsync(b->d_state, 0, sb, b->stream) != hipSuccess ||
         hipMemsetAsync(b->d_nsteps, 0, 8 * n_envs, b->stream) != hipSuccess)
         return bail(fail(PBN_E_HIP, "hipMemset"));
     b->d_image = net->image_on(device);
@@ -653,6 +655,18 @@ int pbn_sync(pbn_batch* b) {
     CHECK_NN(b, "batch");
     SET_DEV(b);
     HIP_TRY(hipStreamSynchronize(b->stream));
+    if (b->fault_check) {
+        // a device-path env launch ran with the grid pool: its outputs reach the caller without a host
+        // read, so a dropped env (a claimed slot whose words never arrived) is reported here
+        b->fault_check = false;
+        int32_t f = 0;
+        HIP_TRY(hipMemcpy(&f, b->d_error + 1, 4, hipMemcpyDeviceToHost));
+        if (f) {
+            HIP_TRY(hipMemset(b->d_error + 1, 0, 4));
+            return fail(PBN_E_HIP, "k_env grid pool: a wait timed out in a device-path launch (an env's outputs "
+                                   "were not written)");
+        }
+    }
     return 0;
 }
 
@@ -1043,6 +1057,26 @@ int pbn_step_replay(pbn_batch* b, const uint32_t* node_idx, const uint64_t* k53,
     HIP_TRY(hipMemcpyAsync(b->s_replay_k.p, k53, 8 * n, hipMemcpyHostToDevice, b->stream));
     if (int rc = step_launch(b, n_updates, 0, 1, b->s_replay_i.p, b->s_replay_k.p)) return rc;
     HIP_TRY(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+int pbn_step_forced(pbn_batch* b, const uint32_t* node_idx, uint32_t n_updates) {
+    CHECK_NN(b, "batch");
+    if (!n_updates) return 0;
+    CHECK_NN(node_idx, "node_idx");
+    const uint64_t n = (uint64_t)n_updates * b->B;
+    const uint32_t lo = (uint32_t)b->net->kind == PBN_KIND_PROB_TABLE ? 1u : 0u;
+    for (uint64_t q = 0; q < n; q++)
+        if (node_idx[q] >= (uint32_t)b->N || node_idx[q] < lo)
+            return fail(PBN_E_RANGE, "forced node index %u outside [%u, %d)", node_idx[q], lo, b->N);
+    SET_DEV(b);
+    if (int rc = b->s_replay_i.ensure(4 * n)) return rc;
+    HIP_TRY(hipMemcpyAsync(b->s_replay_i.p, node_idx, 4 * n, hipMemcpyHostToDevice, b->stream));
+    // replay-mode kernel with no k53 array: update t takes the choice word of Philox step update
+    // update_count + t (the draw pbn_step would use), so the stream stays in step with pbn_step
+    if (int rc = step_launch(b, n_updates, b->update_count, 1, b->s_replay_i.p, nullptr)) return rc;
+    b->update_count += n_updates;
+    HIP_TRY(hipStreamSynchronize(b->stream));  // the staging buffer is reused by the next call
     return 0;
 }
 
@@ -1588,8 +1622,8 @@ static int env_launch(pbn_batch* b, pbn_envcfg* cfg, const int32_t* d_act, int A
             a.gpool_cap = b->env_grid_slots > 0 ? (uint32_t)b->env_grid_slots : GPOOL_CAP;
             a.gpool_epoch = b->gpool_epoch;
             a.gpool_cu_idle = b->env_pool_cu_idle != 0 ? 1u : 0u;
-            a.gpool_migrate = b->env_migrate_blocks >= 0 ? (uint32_t)b->env_migrate_blocks : GPOOL_MIGRATE_BLOCKS;
             b->gpool_last = true;
+            if (d_obs != b->s_obs.p) b->fault_check = true;  // device path: pbn_sync reads the sticky fault word
         }
     }
     hipEvent_t stop;
@@ -1802,7 +1836,7 @@ int pbn_env_grid_stats(pbn_batch* b, uint32_t* stats) {
     CHECK_NN(b, "batch");
     CHECK_NN(stats, "stats");
     SET_DEV(b);
-    for (int k = 0; k < 5; k++) stats[k] = 0;
+    for (int k = 0; k < 4; k++) stats[k] = 0;
     if (!b->gpool_last) return 0;
     HIP_TRY(hipStreamSynchronize(b->stream));
     uint32_t ctl[6];
@@ -1811,7 +1845,6 @@ int pbn_env_grid_stats(pbn_batch* b, uint32_t* stats) {
     stats[1] = ctl[1];  // tickets taken
     stats[2] = ctl[4];  // waits given up
     stats[3] = ctl[2];  // live count at the end (0 after a complete launch)
-    stats[4] = ctl[5];  // of the pushed envs, sessions moved mid-way
     return 0;
 }
 

@@ -325,7 +325,16 @@ void k_step(StepArgs a) {
             to_plane<W>(P, cur);
             for (uint32_t t = 0; t < a.T; ++t) {
                 const uint32_t i = a.replay_node[(uint64_t)t * a.B + e];
-                const uint64_t k53 = a.replay_k53[(uint64_t)t * a.B + e];
+                uint64_t k53;
+                if (a.replay_k53) {
+                    k53 = a.replay_k53[(uint64_t)t * a.B + e];
+                } else {
+                    // forced node (Graph.step(i=k), base.py:306-308): the node is the caller's, the
+                    // choice word is the env's own Philox step draw of update update_base + t
+                    uint32_t wn, wc;
+                    step_words(a.seed, a.update_base + t, a.env_base + e, wn, wc);
+                    k53 = u32_k53(wc);
+                }
                 if constexpr (KIND == KIND_PREDICTOR_MIX)
                     predictor_update_lds(P, i, k53, lds, a.L);
                 else
@@ -879,7 +888,7 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
             const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
             if ((int32_t)(now - gview[2]) < 0) return;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the view loaded at the last look has landed
-            const int32_t waiting = (int32_t)(gview[0] - gview[1]);
+            const int32_t waiting = (int32_t)(min(gview[0], a.gpool_cap) - gview[1]);
             wave_sync();
             if (lane == 0) gview[2] = now + PBN_GPOOL_CHECK_TICKS;
             gview_issue();  // for the next look
@@ -957,14 +966,16 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
         }
         if (__shfl(leave, 0)) return false;
         ticket = (uint32_t)__shfl((int)ticket, 0);
-        const bool has_slot = ticket < a.gpool_cap;
-        gu64* g = (gu64*)(a.gpool + (uint64_t)(has_slot ? ticket : 0u) * GPOOL_GRANULES);
+        // a ticket past the pool's slots can never receive an env: leave at once (pushers count only the
+        // tickets that have slots, so none waits for this one)
+        if (ticket >= a.gpool_cap) return false;
+        gu64* g = (gu64*)(a.gpool + (uint64_t)ticket * GPOOL_GRANULES);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         bool claimed = false;  // the quiet give-up found the slot claimed: its words are on their way
         for (uint32_t it = 0;; ++it) {
             // lane 0 polls the slot's last granule; once it carries the epoch, the whole wave sweeps the slot
             int seen = 0;
-            if (lane == 0 && has_slot)
+            if (lane == 0)
                 seen = (uint32_t)(__hip_atomic_load(g + (NBW - 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == GE;
             if (__shfl(seen, 0)) {
                 for (;;) {
@@ -983,15 +994,15 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                 if (lane == 0) {
                     if (!claimed && __hip_atomic_load(gctl(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
                         // nothing live: no push can come any more -- unless one already claimed this slot
-                        leave = !has_slot || (__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u,
-                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE;
+                        leave = (__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE;
                         claimed = !leave;
                     }
                     const uint64_t waited = __builtin_amdgcn_s_memrealtime() - t0;
                     if (!leave && !claimed && waited > GPOOL_GIVE_UP_TICKS) {
                         // waited long with no env: give the slot up (as above) and leave, unless a push claimed it
-                        if (!has_slot || (__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE)
+                        if ((__hip_atomic_fetch_max((gu32*)(a.gpool_state + ticket), GE << 2 | 2u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) >> 2) != GE)
                             leave = 1;
                         else
                             claimed = true;
@@ -1000,6 +1011,7 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                         leave = 1;
                         (void)__hip_atomic_fetch_add(gctl(4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         atomicOr(a.error, 2);
+                        atomicOr(a.error + 1, 2);  // sticky: device-path launches report it at pbn_sync
                     }
                 }
                 if (__shfl(leave, 0)) return false;
@@ -1037,8 +1049,17 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                                 break;
                             }
                             uint32_t zero = 0u;
-                            if (__hip_atomic_compare_exchange_strong(&wctl[2], &zero, 1u, __ATOMIC_RELAXED,
+                            // acquire: a sibling that got an env from the pool raised the busy count before it
+                            // released this word, so the count re-read below sees it (the count
+                            // read above may predate that increment)
+                            if (__hip_atomic_compare_exchange_strong(&wctl[2], &zero, 1u, __ATOMIC_ACQUIRE,
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                                if (ldl(&wctl[0]) != 0u) {
+                                    // the workgroup is busy again: not idle, keep polling
+                                    __hip_atomic_store(&wctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    __builtin_amdgcn_s_sleep(2);
+                                    continue;
+                                }
                                 if (__hip_atomic_fetch_and(&wctl[1], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
                                     bit) {
                                     got = 3;
@@ -1548,7 +1569,6 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                 }
                 // ring mode (helpers recruited): ringH = the session's helpers (0: self-prepared blocks)
                 uint32_t ringH = 0;
-                bool migrated = false;  // the env went to the grid pool mid-session (lane L holds no env now)
                 uint32_t rblocks = 0, rwaits = 0;  // ring diagnostics (pbn_env_tail_stats)
                 uint32_t* const rcs = rctl_of(wv_in_wg);
                 TailDraw D = prepare(0u);
@@ -1661,24 +1681,11 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                         const uint64_t others = __ballot(e >= 0) & ~(1ull << L);
                         if (others) local_push(others);
                         const bool alone = !(SPLIT && a.tail_helpers && ring_R >= 3u && ldl(&wctl[1]) != 0u);
-                        if (GRID && alone && a.tail_helpers && ring_R >= 3u && a.gpool_migrate && nblk >= a.gpool_migrate) {
-                            // a long session no idle sibling can help: the env itself moves to a CU that has run
-                            // out of work, whose idle waves become its helpers (0.41 vs 0.7-0.85 us per 64
-                            // updates); its words as the session has them (used, counters; the plane is committed)
-                            if (lane == L) {
-                                used = u;
-                                m_lo = m;
-                            }
-                            grid_push(1ull << L);
-                            if (__shfl((int)(e < 0), (int)L)) {
-                                migrated = true;
-                                if (lane == 0)
-                                    (void)__hip_atomic_fetch_add(gctl(5), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                return;
-                            }
-                        }
                         if (others) grid_push(__ballot(e >= 0) & ~(1ull << L));
-                        if (!alone) {
+                        // (a ring starts at an even update: helpers key a pair's Philox call by u >> 1 -- always so
+                        // here, lane mode and the hand-offs start sessions at multiples of the draw chunk and a
+                        // block advances u by 64 unless the session ends; an odd start keeps self-prepared blocks)
+                        if (!alone && (u & 1u) == 0u) {
                             const uint32_t cl = claim_idle(min((uint32_t)a.tail_helpers, 3u));
                             if (cl) {
                                 const uint32_t H = (uint32_t)__popc(cl);
@@ -1902,7 +1909,7 @@ __global__ __launch_bounds__(ENV_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
                     est[39] = sess_u0;
                 }
 #endif
-                if (lane == L && !migrated) {
+                if (lane == L) {
                     used = u;
                     m_lo = m;
                     capped = !hitf;

@@ -63,7 +63,7 @@ struct StepArgs {
     uint64_t update_base;        // Philox update counter of the first update
     uint32_t T;                  // updates per launch
     const uint32_t* replay_node; // [T][B] (replay mode)
-    const uint64_t* replay_k53;  // [T][B]
+    const uint64_t* replay_k53;  // [T][B]; null: forced nodes, choice words from the Philox step stream
     int32_t grp;                 // rollout: lanes per env (1 = k_rollout; 2/4/8 = k_rollout_grp)
     const uint64_t* ubase_dev;   // step mode in a HIP graph: update counter = *ubase_dev + update_base
 };
@@ -147,8 +147,6 @@ struct EnvArgs {
     uint32_t gpool_epoch;     // this launch's tag (1 .. 2^30 - 1, a new one per launch)
     uint32_t gpool_cu_idle;   // 1: a workgroup takes tickets only once no workgroup of its CU is on its own envs;
                               // 0: as soon as its own waves have run out of work
-    uint32_t gpool_migrate;   // a tail session that has run this many blocks with no idle sibling to help it moves
-                              // itself into the pool (0 = never; GPOOL_MIGRATE_BLOCKS by default)
 };
 
 constexpr uint32_t GPOOL_GRANULES = 64;  // per slot: the hand-off box as u32 words (10 + 4W <= 64 for W <= 13)
@@ -160,9 +158,6 @@ constexpr uint32_t GPOOL_CU_WORD = 16, GPOOL_CTL_BYTES = 4u * (GPOOL_CU_WORD + 1
 // this (pbn_abi.cpp env_launch): one env step at config 5's 4,096 cap lost more to the waiting workgroups'
 // residency than the moved envs gave back (1.14 -> 1.18-1.20 ms per step)
 constexpr uint32_t GPOOL_MIN_CAP = 16384;
-// sessions moved mid-way: 16 / 64 / 256 blocks / never measured within run-to-run noise of each other at config 5's
-// shard (profiles/r05_r6_grid_pool_ab.json "migrate_threshold"); 256 keeps it to the longest sessions
-constexpr uint32_t GPOOL_MIGRATE_BLOCKS = 256;
 
 constexpr uint32_t MT_ROW = 624;
 

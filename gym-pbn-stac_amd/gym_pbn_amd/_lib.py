@@ -102,6 +102,7 @@ SIGNATURES = {
     "pbn_step_prepare": (C.c_int, [_vp, C.c_uint32]),
     "pbn_rollout": (C.c_int, [_vp, C.c_uint32]),
     "pbn_step_replay": (C.c_int, [_vp, _u32p, _u64p, C.c_uint32]),
+    "pbn_step_forced": (C.c_int, [_vp, _u32p, C.c_uint32]),
     "pbn_mt_seed": (C.c_int, [_vp, _u64p, C.c_int]),
     "pbn_mt_step": (C.c_int, [_vp, C.c_uint32]),
     "pbn_envcfg_create": (C.c_int, [_vp, C.POINTER(EnvCfgDesc), _PP]),

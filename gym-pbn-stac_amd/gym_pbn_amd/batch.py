@@ -291,6 +291,12 @@ class PBNBatch:
             raise ValueError("node_idx and k53 shapes differ")
         L.check(L.lib.pbn_step_replay(self._h, L.ptr(ni, L._u32p), L.ptr(kk, L._u64p), ni.shape[0]))
 
+    def step_forced(self, node_idx):
+        """Updates with caller-chosen nodes (``node_idx`` ``[T][B]``) and the Philox choice draws
+        ``step`` would use for those updates; the update counter advances by T (pbn_step_forced)."""
+        ni = np.ascontiguousarray(node_idx, dtype=np.uint32).reshape(-1, self.n_envs)
+        L.check(L.lib.pbn_step_forced(self._h, L.ptr(ni, L._u32p), ni.shape[0]))
+
     def mt_seed(self, seeds, init_state: bool = True):
         s = np.ascontiguousarray(seeds, dtype=np.uint64).reshape(self.n_envs)
         L.check(L.lib.pbn_mt_seed(self._h, L.ptr(s, L._u64p), int(bool(init_state))))
@@ -419,10 +425,10 @@ class PBNBatch:
 
     def env_grid_stats(self) -> dict:
         """The last R6 launch's grid-pool counters: envs handed to workgroups that had run out of work,
-        tickets those workgroups took, waits given up (0), live count at the end (0), sessions moved mid-way."""
-        st = (C.c_uint32 * 5)()
+        tickets those workgroups took, waits given up (0), live count at the end (0)."""
+        st = (C.c_uint32 * 4)()
         L.check(L.lib.pbn_env_grid_stats(self._h, st))
-        return {"pushed": st[0], "tickets": st[1], "gave_up": st[2], "live_at_end": st[3], "migrated": st[4]}
+        return {"pushed": st[0], "tickets": st[1], "gave_up": st[2], "live_at_end": st[3]}
 
     def env_handoffs(self) -> int:
         """Envs the last R6 launch handed from tail-mode waves to idle ones (0 with the hand-off off)."""

@@ -77,9 +77,16 @@ class Graph:
     def step(self, changed_nodes=None, i=None) -> tuple:  # base.py:306-312 (changed_nodes is ignored there too)
         if not self._initialised:
             raise Exception("Forgot to initialise the states")  # base.py:90-91
-        if i is not None:
-            raise NotImplementedError("a forced node index is not supported by the Philox device stream")
-        self._b.step(1)
+        if i is None:
+            self._b.step(1)
+        else:
+            # base.py:307-309: `self.nodes[i]` -- Python list indexing (negative i counts from the
+            # end, anything else out of range raises IndexError); no node draw is made, the
+            # predictor choice is this update's Philox choice draw
+            i = int(i)
+            if not -self.N <= i < self.N:
+                raise IndexError("list index out of range")
+            self._b.step_forced(np.array([[i % self.N]], dtype=np.uint32))
         return self.getState()
 
 

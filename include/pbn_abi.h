@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 13
+#define PBN_ABI_VERSION 14
 
 enum {
     PBN_OK = 0,
@@ -143,6 +143,7 @@ int pbn_net_select_u32(const pbn_net *net, int32_t node, uint32_t a, uint64_t *r
  * PBNSIM_STORE_MODE, PBNSIM_ENVS_PER_THREAD, PBNSIM_STEP_BLOCK (step kernel);
  * PBNSIM_ENV_NO_GEN, PBNSIM_ENV_GROUP, PBNSIM_ENV_BPC, PBNSIM_ENV_CHUNK, PBNSIM_ENV_GRID, PBNSIM_ENV_TAIL,
  * PBNSIM_ENV_LANES, PBNSIM_ENV_STEAL, PBNSIM_ENV_HELPERS, PBNSIM_ENV_GRID_STEAL, PBNSIM_ENV_KERNEL_IMAGE (R6 env kernel);
+ * every one is set by a `-m gpu` test; A/B-only knobs are compiled in by -DPBN_MEASURE_KNOBS (tools/build_exp.sh);
  * PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL, PBNSIM_SSD_SHARED (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
  * PBNSIM_STEP_GRAPH=0 (pbn_step without HIP graphs). */
 int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
@@ -153,6 +154,8 @@ int pbn_batch_get_info(const pbn_batch *b, pbn_batch_info *info);
  * kernels order with the caller's own work without host syncs; NULL = the default stream), or on
  * the batch's own stream again (own != 0). Work queued on the previous stream is waited for first. */
 int pbn_batch_set_stream(pbn_batch *b, int own, void *stream);
+/* Waits for the batch stream. PBN_E_HIP if a device-path R6 launch since the last pbn_sync dropped an env in
+ * the grid pool (see pbn_env_grid_stats; never expected). */
 int pbn_sync(pbn_batch *b);
 
 /* ---- state I/O: Graph.setState / getState (base.py:364-366, 320-324), PBN.reset(state) (pbn.py:96-119) ---- */
@@ -197,6 +200,12 @@ int pbn_step_prepare(pbn_batch *b, uint32_t n_updates);
 int pbn_rollout(pbn_batch *b, uint32_t n_updates);
 /* Replay mode: node_idx [T][B] (randint result) and k53 [T][B] (random() * 2^53), host arrays. */
 int pbn_step_replay(pbn_batch *b, const uint32_t *node_idx, const uint64_t *k53, uint32_t n_updates);
+/* Forced node (replaces Graph.step(i=k), base.py:306-308: `i = randint(...) if i is None else i`):
+ * node_idx [T][B] host array (PROB_TABLE: >= 1); update t of env e updates node node_idx[t][e] with
+ * the choice word of the Philox step draw pbn_step would have used for that update (its node word
+ * is discarded), and the batch's update counter advances by T like pbn_step's. Out-of-range
+ * indices: PBN_E_RANGE, nothing launched. Synchronous. */
+int pbn_step_forced(pbn_batch *b, const uint32_t *node_idx, uint32_t n_updates);
 /* MT mode: seeds [B] (host). random.seed(seeds[e]) (and np.random.seed for PROB_TABLE).
  * init_state 1 also runs Graph.genRandState / PBN.reset(None) from that stream. */
 int pbn_mt_seed(pbn_batch *b, const uint64_t *seeds, int init_state);
@@ -265,11 +274,12 @@ int pbn_env_tail_helpers(pbn_batch *b, uint32_t *count);
  * sessions read from their helpers' rings, and of those the blocks not yet written when the session reached
  * them (the session waited). Syncs the batch stream. Diagnostics. */
 int pbn_env_tail_stats(pbn_batch *b, uint32_t *stats);
-/* The last R6 launch's grid-pool counters, stats[5] (env_kernel 4 with the hand-off on; on by default for fused
+/* The last R6 launch's grid-pool counters, stats[4] (env_kernel 4 with the hand-off on; on by default for fused
  * launches and update caps >= 16,384, PBNSIM_ENV_GRID_STEAL=0/1 forces it): envs a tail wave handed to a workgroup
  * that had run out of work (anywhere on the GPU), tickets those workgroups took, waits given up (0 unless a launch
- * failed with PBN_E_HIP), the live count at the launch's end (0), and of the envs handed over, sessions moved
- * mid-way (a long tail session no idle sibling could help). Syncs the batch stream. Diagnostics. */
+ * failed with PBN_E_HIP), the live count at the launch's end (0). Syncs the batch stream. Diagnostics. A given-up
+ * wait drops the env it waited for: host-path env calls return PBN_E_HIP at once, device-path launches
+ * (pbn_env_step_multi_device, pbn_env_rollout_multi_device) at the next pbn_sync. */
 int pbn_env_grid_stats(pbn_batch *b, uint32_t *stats);
 
 #ifdef __cplusplus

@@ -268,6 +268,24 @@ EXPORT int orc_step_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_
     return 0;
 }
 
+/* Graph.step(i=k) (base.py:306-309: the node is the caller's, no randint draw): update t of env e
+ * updates node node_idx[t][e] with the choice word of Philox step update update_base + t (the node
+ * word of that call is unused) -- the device's pbn_step_forced. */
+EXPORT int orc_step_forced(const orc_net *n, uint64_t *state, int64_t B, uint64_t seed, uint64_t env_base,
+                           uint64_t update_base, const uint32_t *node_idx, int T) {
+    const int W = n->n_words;
+    for (int t = 0; t < T; t++)
+        for (int64_t e = 0; e < B; e++) {
+            uint32_t i = node_idx[(int64_t)t * B + e];
+            if ((int)i >= n->n_nodes) return -2;
+            uint64_t u = update_base + (uint64_t)t, g = env_base + (uint64_t)e;
+            uint32_t w[4];
+            philox_draw(seed, (uint32_t)u, (uint32_t)(u >> 32), g >> 1, STREAM_STEP, w);
+            node_update(n, state + e * W, (int)i, u32_k53(w[2 * (int)(g & 1u) + 1]));
+        }
+    return 0;
+}
+
 /* genRandState analogue for the Philox mode: fair bits, bits >= N cleared;
  * probability-table networks also clear node 0 (pbn.py:118). */
 EXPORT void orc_init_philox(const orc_net *n, uint64_t *state, int64_t B, uint64_t seed, uint64_t env_base,
@@ -373,19 +391,25 @@ static inline int action_node(int a, int offset, int N, int *node) {
 }
 
 /* rng_mode 0 = replay (draw_off [B+1], draws_i/draws_k), 1 = philox (seed, env_base, call_idx).
+ * n_threads > 0: OpenMP threads over the envs (0: the OpenMP default).
  * flags bit0 terminated, bit1 truncated, bit2 capped. Returns -2 on an invalid action
  * (checked for every env before any state changes). */
 EXPORT int orc_env_step_multi(const orc_net *n, const orc_envcfg *c, uint64_t *state, int64_t *n_steps, int64_t B,
                               const int32_t *actions, int A, int dedup, int offset, int rng_mode,
                               const int64_t *draw_off, const uint32_t *draws_i, const uint64_t *draws_k,
                               uint64_t seed, uint64_t env_base, uint32_t call_idx, uint32_t update_cap,
-                              uint64_t *obs, int32_t *reward, uint8_t *flags, uint32_t *n_updates) {
+                              uint64_t *obs, int32_t *reward, uint8_t *flags, uint32_t *n_updates, int n_threads) {
     const int W = n->n_words, N = n->n_nodes;
     for (int64_t e = 0; e < B; e++)
         for (int k = 0; k < A; k++) {
             int a = actions[e * A + k], node;
             if (a != 0 && action_node(a, offset, N, &node)) return -2;
         }
+    /* envs are independent; loop lengths vary by orders of magnitude, hence the dynamic schedule */
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
     for (int64_t e = 0; e < B; e++) {
         uint64_t *s = state + e * W;
         const int32_t *act = actions + e * A;

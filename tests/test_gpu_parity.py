@@ -52,6 +52,56 @@ def test_single_env_b1_plumbing(G):
         assert np.array_equal(b.get_state()[0], z["states"][0, t])
 
 
+@pytest.mark.parametrize("name,B,base", [("bittner199", 4099, 77), ("bittner28", 1024, 64), ("tt200", 2048, 9)])
+def test_step_forced_matches_oracle(G, oracle_mod, name, B, base):
+    """``Graph.step(i=k)`` (base.py:306-309): the caller's node, the Philox choice draw of that update;
+    forced updates interleave with ``step`` / ``rollout`` on one update counter."""
+    net = load_network(name)
+    o = oracle_mod.Oracle(net)
+    b = G.PBNBatch(net, B, seed=99, env_id_base=base)
+    b.randomize()
+    st = b.get_state()
+    lo = 1 if net.kind == 2 else 0
+    ni = np.random.default_rng(B).integers(lo, net.n_nodes, size=(5, B)).astype(np.uint32)
+    b.step_forced(ni)
+    st = o.step_forced(st, ni, 99, base, 0)
+    assert np.array_equal(b.get_state(), st)
+    b.step(3)  # continues at update 5
+    st = o.step_philox(st, 99, base, 5, 3)
+    assert np.array_equal(b.get_state(), st)
+    b.step_forced(ni[:1])  # update 8
+    assert np.array_equal(b.get_state(), o.step_forced(st, ni[:1], 99, base, 8))
+    with pytest.raises(Exception):
+        b.step_forced(np.full((1, B), net.n_nodes, np.uint32))
+
+
+def test_graph_step_forced_node(G, oracle_mod):
+    """Single env: ``Graph.step(i=k)`` changes at most node k, equals the oracle, takes Python list
+    indexing (negative k) and raises IndexError out of range like ``self.nodes[i]``."""
+    from gym_pbn_amd.envs import Graph
+
+    net = load_network("bittner199")
+    o = oracle_mod.Oracle(net)
+    g = Graph(net, seed=5, env_id=3)
+    g.genRandState()
+    words = o.init_philox(1, seed=5, env_base=3)
+    assert g.getState() == tuple(oracle_mod.unpack_bits(words, net.n_nodes)[0].tolist())
+    u = 0
+    for k in [0, 17, 198, -1, -199, 42, 42, 42]:
+        s0 = g.getState()
+        s1 = g.step(i=k)
+        node = k % net.n_nodes
+        assert all(a == b for j, (a, b) in enumerate(zip(s0, s1)) if j != node)
+        words = o.step_forced(words, np.array([[node]], np.uint32), 5, 3, u)
+        u += 1
+        assert s1 == tuple(oracle_mod.unpack_bits(words, net.n_nodes)[0].tolist()), k
+    s = g.step()  # the unforced step draws update u's node
+    assert s == tuple(oracle_mod.unpack_bits(o.step_philox(words, 5, 3, u, 1), net.n_nodes)[0].tolist())
+    for bad in (199, -200):
+        with pytest.raises(IndexError):
+            g.step(i=bad)
+
+
 # ----------------------------------------------------------------- Philox mode vs oracle
 # an even env base puts envs 2m / 2m + 1 (which share a Philox call) in lane pairs that swap words
 # over DPP; an odd base takes the one-call-per-env path
@@ -108,6 +158,22 @@ def test_step_graph_replays_match_oracle(G, oracle_mod, monkeypatch, graph, name
         assert b.timing_read()[1] == n
         done += n
         assert np.array_equal(b.get_state(), o.step_philox(init, 71, 13, 0, done)), n
+    b.close()
+
+
+@pytest.mark.parametrize("block", ["256", "1024"])
+def test_step_block_sizes_match_oracle(G, oracle_mod, monkeypatch, block):
+    """Step mode with the workgroup size forced (PBNSIM_STEP_BLOCK: 1,024-thread groups are picked for
+    batches that fill the GPU, 256 below): both sizes at a ragged batch, every env against the oracle."""
+    monkeypatch.setenv("PBNSIM_STEP_BLOCK", block)
+    net = load_network("bittner199")
+    o = oracle_mod.Oracle(net)
+    B = 300001
+    b = G.PBNBatch(net, B, seed=17, env_id_base=5)
+    b.randomize()
+    init = b.get_state()
+    b.step(7)
+    assert np.array_equal(b.get_state(), o.step_philox(init, 17, 5, 0, 7, n_threads=16))
     b.close()
 
 
@@ -604,7 +670,8 @@ def test_mt_mode_truth_table_reproduces_reference(G, name):
 
 
 def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
-    """65,536 envs seeded 0..65535 (crossing many MT twists); sampled envs vs the oracle's CPython MT."""
+    """65,536 envs with spread seeds (crossing many MT twists, rows running out in different iterations):
+    EVERY env vs the oracle's CPython MT (OpenMP over the envs)."""
     net = load_network("bittner199")
     B, T = 65536, 700
     seeds = np.arange(B, dtype=np.uint64) * np.uint64(2654435761) + np.uint64(3)
@@ -612,11 +679,27 @@ def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
     b.mt_seed(seeds, init_state=True)
     b.mt_step(T)
     got = b.get_state()
+    b.close()
     o = oracle_mod.Oracle(net)
-    idx = np.random.default_rng(1).choice(B, 64, replace=False)
-    assert np.array_equal(got[idx], o.run_mt(seeds[idx], T))
+    assert np.array_equal(got, o.run_mt(seeds, T, n_threads=16))
     with pytest.raises(ValueError):
         G.PBNBatch("tt8", 2).mt_seed(np.array([1, 2**33], dtype=np.uint64))
+
+
+def test_mt_mode_bench_workload_vs_oracle(G, oracle_mod):
+    """bench.py's MT workload itself (mt_supplement: Bittner-199, 1,048,576 envs seeded 12345 + id, the
+    state from genRandState, T = 256 updates per pbn_mt_step launch): two launches, every env vs the oracle's
+    run_mt from the seeds alone (16 threads)."""
+    net = load_network("bittner199")
+    B, T = 1 << 20, 256
+    seeds = np.arange(B, dtype=np.uint64) + np.uint64(12345)
+    b = G.PBNBatch(net, B, seed=1)
+    b.mt_seed(seeds, init_state=True)
+    b.mt_step(T)
+    b.mt_step(T)
+    got = b.get_state()
+    b.close()
+    assert np.array_equal(got, oracle_mod.Oracle(net).run_mt(seeds, 2 * T, n_threads=16))
 
 
 # ----------------------------------------------------------------- config 5: device trajectory chunks

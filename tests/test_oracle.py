@@ -149,3 +149,42 @@ def test_philox_transition_statistics(oracle_mod):
         expect = B / net.n_nodes * (p if x[i] == 0 else 1 - p)
         assert abs(flips - expect) <= 5 * np.sqrt(expect + 1) + 2, (i, flips, expect)
     assert changed_node.shape == (B,)
+
+
+@pytest.mark.parametrize("name", ["bittner199", "tt200"])
+def test_forced_step_with_the_drawn_nodes_is_the_philox_step(oracle_mod, name):
+    """``orc_step_forced`` (Graph.step(i=k)) fed the nodes the Philox step would draw (``mulhi(w, N)`` /
+    ``1 + mulhi(w, N - 1)`` of the node word) reproduces ``orc_step_philox``: the choice word is the same."""
+    net = load_network(name)
+    o = oracle_mod.Oracle(net)
+    B, T, seed, base = 257, 6, 31, 1001
+    st = o.init_philox(B, seed=seed, env_base=base)
+    ni = np.zeros((T, B), np.uint32)
+    for t in range(T):
+        for e in range(B):
+            g = base + e
+            w = oracle_mod.philox4x32_10([t, 0, (g >> 1) & 0xFFFFFFFF, ((g >> 1) >> 32) | (1 << 24)],
+                                         [seed & 0xFFFFFFFF, seed >> 32])
+            wn = w[2 * (g & 1)]
+            ni[t, e] = (wn * net.n_nodes) >> 32 if net.kind == 1 else 1 + ((wn * (net.n_nodes - 1)) >> 32)
+    assert np.array_equal(o.step_forced(st, ni, seed, base, 0), o.step_philox(st, seed, base, 0, T))
+    # another node sequence gives another trajectory
+    assert not np.array_equal(o.step_forced(st, (ni + 1) % net.n_nodes | (net.kind == 2), seed, base, 0),
+                              o.step_philox(st, seed, base, 0, T))
+
+
+def test_env_step_multi_threads_do_not_change_results(oracle_mod):
+    """The OpenMP env loop of ``orc_env_step_multi`` gives the single-threaded results."""
+    net = load_network("bittner28")
+    z = golden("r6_bittner28.npz")
+    cfg = r6_config(z)
+    o = oracle_mod.Oracle(net)
+    B = 3000
+    st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.zeros(B, np.int64), cfg["reset_care"],
+                                cfg["reset_value"], seed=4, env_base=11)
+    rng = np.random.default_rng(4)
+    acts = rng.integers(0, net.n_nodes + 1, size=(B, 2)).astype(np.int32)
+    r1 = o.env_step_multi(cfg, st, ns, acts, seed=4, env_base=11, update_cap=4096, n_threads=1)
+    r4 = o.env_step_multi(cfg, st, ns, acts, seed=4, env_base=11, update_cap=4096, n_threads=4)
+    for k in r1:
+        assert np.array_equal(r1[k], r4[k]), k

@@ -8,7 +8,9 @@ come from, checked against the oracle (``oracle.env_step_multi``, the CPU restat
   waves start full (>= 40 active lanes: each lane draws its own entries) and end in the tail
   (< 40: the rank / counter tables of the shared path). All envs are compared.
 * Config 5 per GPU: 131,072 Bittner-199 envs, one T = 100 chunk in one fused launch, equal in
-  full to 100 per-step launches and to the oracle on 2,000 sampled envs.
+  full to 100 per-step launches and, on every env, field and step, to the oracle; the same shard at
+  the reference-faithful cap 2^20 for both attractor specs (per step and fused, library defaults:
+  grid pool, tail helpers, hand-off), every env against the oracle.
 
 Production settings: the r6_bittner199 fixture's attractor cubes, A = 4 (0 w.p. 0.75),
 update cap 4,096 (about a fifth of the env steps run into it).
@@ -52,16 +54,19 @@ def G():
 
 
 @pytest.mark.parametrize("mode", ["per_step", "fused", "grp8_per_step", "one_lane_per_step", "one_lane_fused",
-                                  "per_step_chunk32", "fused_chunk32", "per_step_kernel_image"])
+                                  "per_step_chunk32", "fused_chunk32", "per_step_kernel_image", "fused_bpc1"])
 def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
     """... and with either draw-round chunk (EnvArgs::chunk: 48 for these launches, 32 forced by
     PBNSIM_ENV_CHUNK -- the chunk the host picks for long fused launches over large batches); and with
     the kernel building its LDS image itself (PBNSIM_ENV_KERNEL_IMAGE=1) instead of staging the
-    host-built one (pbn_abi.cpp env_gen_image), so both constructions stay exact."""
+    host-built one (pbn_abi.cpp env_gen_image), so both constructions stay exact; and with the workgroups per CU
+    capped at one (PBNSIM_ENV_BPC=1)."""
     import torch
 
     if mode.endswith("kernel_image"):
         monkeypatch.setenv("PBNSIM_ENV_KERNEL_IMAGE", "1")
+    if mode.endswith("bpc1"):
+        monkeypatch.setenv("PBNSIM_ENV_BPC", "1")  # one workgroup per CU (the occupancy the host sizes against)
 
     grp = "8" if mode.startswith("grp8") else "1"
     chunk32 = mode.endswith("chunk32")
@@ -115,19 +120,45 @@ def test_lane_refill_matches_oracle(G, oracle_mod, monkeypatch, mode):
     assert 0 < capped < T * B  # both regimes: envs that hit the cap and envs that reached an attractor
 
 
-def test_config5_chunk_131k_fused_vs_per_step_and_oracle(G, oracle_mod):
-    """BASELINE config 5's per-GPU shard: 131,072 envs, T = 100 env steps. The fused chunk (one
-    launch) equals 100 per-step launches on every env and field; 2,000 envs (20 blocks of 100 at
-    random offsets) equal the oracle step by step."""
+_C5 = {}  # config 5's shard per bench figure, computed once: device outputs, then the oracle's progress through them
+_C5_PARTS = 4
+# bench.py's three config-5 figures (r6_supplement): the headline (fixture cubes, cap 4,096), high_cap and
+# spec_attractors (cap 2^20, R6_HIGH_CAP)
+_C5_FIGURES = [("fixture", CAP), ("fixture", 1 << 20), ("spec", 1 << 20)]
+
+
+def _config5_device(G, spec, cap):
+    """Config 5's shard as bench.py runs it (r6_figure): 131,072 envs of rank 3 of the 8-GPU run (global ids
+    3 * 131,072 ...), actions from ``actions.env_actions`` (Philox 0xAC7 keyed by global env id), T = 100,
+    library defaults. One fused T = 100 launch (grid pool on) and 100 per-step launches of a second batch
+    (pool on from cap 16,384), which must agree on every env and field; host copies of the fused outputs are
+    kept for the oracle parts."""
+    key = (spec, cap)
+    if key in _C5:
+        return _C5[key]
+    import sys
+    from pathlib import Path
+
     import torch
 
-    B, T, A, seed, base = 131072, 100, 4, 0xAC7, 3 * 131072  # rank 3 of 8
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    from gym_pbn_amd.actions import env_actions
+
+    _C5.clear()  # one figure's host copies at a time
+    B, T, A, seed, base = 131072, 100, 4, 0xAC7, 3 * 131072
     dev = torch.device("cuda", 0)
-    net, cfg, cfgd, b1 = _setup(G, B, seed, base)
+    net = load_network("bittner199")
+    gnet = G.Net(net)
+    atts, _ = bench.r6_attractors(spec, net.n_nodes)
+    cfg = G.EnvConfig(gnet, atts, horizon=T)
+    cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
+                horizon=T)
+    d_a = env_actions(T, base, B, A, net.n_nodes, seed=0xAC7, device=dev)
+    b1 = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
+    b1.env_reset(cfg)
     init = b1.get_state()
     ns0 = b1.get_n_steps()
-    acts = _actions(np.random.default_rng(99), (T, B, A), net.n_nodes)
-    d_a = torch.from_numpy(acts).to(dev)
 
     def outs():
         return (torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev),
@@ -136,36 +167,69 @@ def test_config5_chunk_131k_fused_vs_per_step_and_oracle(G, oracle_mod):
                 torch.empty((T, B), dtype=torch.int32, device=dev))
 
     fo = outs()
-    b1.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, *[x.data_ptr() for x in fo], update_cap=CAP)
-    b1.sync()
-    b2 = G.PBNBatch(cfg.net, B, seed=seed, env_id_base=base)
+    b1.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, *[x.data_ptr() for x in fo], update_cap=cap)
+    b1.sync()  # raises if the pool dropped an env
+    pools = [b1.env_grid_stats()]
+    b2 = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
     b2.env_reset(cfg)
     po = outs()
     for t in range(T):
-        b2.env_step_multi_device(cfg, d_a[t].data_ptr(), A, *[x[t].data_ptr() for x in po], update_cap=CAP)
+        b2.env_step_multi_device(cfg, d_a[t].data_ptr(), A, *[x[t].data_ptr() for x in po], update_cap=cap)
+        if t % 10 == 9:
+            pools.append(b2.env_grid_stats())
     b2.sync()
     for x, y in zip(fo, po):
         assert torch.equal(x, y)
     assert np.array_equal(b1.get_state(), b2.get_state()) and np.array_equal(b1.get_n_steps(), b2.get_n_steps())
-    flags = fo[2].cpu().numpy()
-    nup = fo[3].cpu().numpy()
-    assert (flags[-1] & 2).all()  # truncated at the horizon
-    assert 0.05 < ((flags & 4) != 0).mean() < 0.5 and nup.max() == CAP  # the capped regime is exercised
-    # oracle on 2,000 sampled envs
-    o = oracle_mod.Oracle(net)
-    obs, rew, fl = fo[0].cpu().numpy().view(np.uint64), fo[1].cpu().numpy(), flags
-    starts = np.sort(np.random.default_rng(5).choice(B // 100, 20, replace=False)) * 100
-    for s0 in starts:
-        sl = slice(int(s0), int(s0) + 100)
-        st, ns = init[sl], ns0[sl]
-        for t in range(T):
-            ref = o.env_step_multi(cfgd, st, ns, acts[t, sl], seed=seed, env_base=base + int(s0), call_idx=t,
-                                   update_cap=CAP)
-            assert np.array_equal(nup[t, sl].view(np.uint32), ref["n_updates"]), (s0, t)
-            assert np.array_equal(obs[t, sl], ref["obs"]) and np.array_equal(rew[t, sl], ref["reward"]), (s0, t)
-            assert np.array_equal(fl[t, sl], ref["flags"]), (s0, t)
-            st, ns = ref["state"], ref["n_steps"]
-        assert np.array_equal(b1.get_state()[sl], st)
+    c = dict(net=net, cfgd=cfgd, B=B, T=T, seed=seed, base=base, cap=cap, acts=d_a.cpu().numpy(), pools=pools,
+             obs=fo[0].cpu().numpy().view(np.uint64), rew=fo[1].cpu().numpy(), flags=fo[2].cpu().numpy(),
+             nup=fo[3].cpu().numpy().view(np.uint32), final=b1.get_state(), final_ns=b1.get_n_steps(),
+             orc_t=0, orc_st=init, orc_ns=ns0)
+    b1.close()
+    b2.close()
+    _C5[key] = c
+    return c
+
+
+@pytest.mark.parametrize("spec,cap", _C5_FIGURES)
+def test_config5_chunk_131k_fused_equals_per_step(G, spec, cap):
+    """BASELINE config 5's per-GPU shard (131,072 envs, rank 3's global ids, T = 100 env steps, the bench's
+    actions) for each of bench.py's three figures: the fused chunk (one launch, grid pool on) equals 100
+    per-step launches on every env and field; the pool moved envs and dropped none."""
+    c = _config5_device(G, spec, cap)
+    assert (c["flags"][-1] & 2).all()  # truncated at the horizon
+    if cap == CAP:
+        assert 0.05 < ((c["flags"] & 4) != 0).mean() < 0.5 and c["nup"].max() == CAP  # the capped regime
+    else:
+        assert not (c["flags"] & 4).any()  # the reference's unbounded loop is never cut
+    assert all(p["gave_up"] == 0 and p["live_at_end"] == 0 for p in c["pools"]), c["pools"]
+    assert c["pools"][0]["pushed"] > 0, c["pools"]  # the fused launch moved envs between workgroups
+    if cap >= 16384:
+        assert sum(p["pushed"] for p in c["pools"][1:]) > 0, c["pools"]  # ... and so did per-step launches
+
+
+@pytest.mark.parametrize("part", range(_C5_PARTS))
+@pytest.mark.parametrize("spec,cap", _C5_FIGURES)
+def test_config5_chunk_131k_every_env_vs_oracle(G, oracle_mod, spec, cap, part):
+    """... and EVERY env of it equals the oracle (OpenMP over the envs) on every field of every env step:
+    steps [25 part, 25 part + 25) here (a part run alone first advances the oracle through the earlier steps;
+    the whole figure takes ~40 s of the box's 16 threads)."""
+    c = _config5_device(G, spec, cap)
+    o = oracle_mod.Oracle(c["net"])
+    per = c["T"] // _C5_PARTS
+    t0, t1 = part * per, (part + 1) * per
+    while c["orc_t"] < t1:
+        t = c["orc_t"]
+        ref = o.env_step_multi(c["cfgd"], c["orc_st"], c["orc_ns"], c["acts"][t], seed=c["seed"], env_base=c["base"],
+                               call_idx=t, update_cap=cap)
+        if t >= t0:
+            assert np.array_equal(c["nup"][t], ref["n_updates"]), t
+            assert np.array_equal(c["obs"][t], ref["obs"]), t
+            assert np.array_equal(c["rew"][t], ref["reward"]), t
+            assert np.array_equal(c["flags"][t], ref["flags"]), t
+        c["orc_st"], c["orc_ns"], c["orc_t"] = ref["state"], ref["n_steps"], t + 1
+    if t1 == c["T"]:
+        assert np.array_equal(c["final"], c["orc_st"]) and np.array_equal(c["final_ns"], c["orc_ns"])
 
 
 def test_collector_does_not_reuse_a_buffer_still_being_gathered(G):
@@ -231,14 +295,18 @@ def test_collector_does_not_reuse_a_buffer_still_being_gathered(G):
 
 
 @pytest.mark.parametrize("spec", ["fixture", "spec"])
-def test_high_cap_matches_oracle(G, oracle_mod, spec):
-    """The loop the reference runs unbounded (pbn_target_multi.py:135-146) at a cap it never
-    reaches in measurement (bench.py R6_HIGH_CAP, 2^20; the longest loop measured at config 5 ran
-    78,057 updates, profiles/r03_r6_cap_sweep.json), for both attractor specs bench.py reports: the
-    fixture's cubes and SURVEY §8(d)'s 4 cubes over the 7 target genes. 8,192 envs x 3 env steps,
-    every env against the oracle; no env is capped."""
+def test_high_cap_full_shard_matches_oracle(G, oracle_mod, spec):
+    """The loop the reference runs unbounded (pbn_target_multi.py:135-146) at the cap bench.py reports it at
+    (R6_HIGH_CAP, 2^20; the longest loop measured at config 5 ran 78,057 updates, profiles/r03_r6_cap_sweep.json),
+    for both attractor specs the bench line carries -- the fixture's cubes and SURVEY §8(d)'s 4 cubes over the 7
+    target genes -- on config 5's whole shard (131,072 envs, rank 3's global ids) at the library defaults (tail
+    helpers, the workgroup hand-off and the grid pool all on): 3 per-step launches and, on a second batch, one
+    fused T = 3 launch; every env and field of both against the oracle, no env capped, and the grid pool moved
+    envs between workgroups in the launches (pushed > 0, nothing given up, live count 0 at the end)."""
     import sys
     from pathlib import Path
+
+    import torch
 
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     import bench
@@ -249,25 +317,47 @@ def test_high_cap_matches_oracle(G, oracle_mod, spec):
     cfg = G.EnvConfig(gnet, atts, horizon=100)
     cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
                 horizon=100)
-    B, seed, base, T, A = 8192, 0xAC7, 40000, 3, 4
+    B, seed, base, T, A = 131072, 0xAC7, 3 * 131072, 3, 4
+    cap = bench.R6_HIGH_CAP
+    acts = _actions(np.random.default_rng(123), (T, B, A), net.n_nodes)
     b = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
     b.env_reset(cfg)
     o = oracle_mod.Oracle(net)
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
     assert np.array_equal(b.get_state(), st)
-    acts = _actions(np.random.default_rng(123), (T, B, A), net.n_nodes)
+    got, pools = [], []
     for t in range(T):
-        obs, rew, flags, nup = b.env_step_multi(cfg, acts[t], update_cap=bench.R6_HIGH_CAP)
-        ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t,
-                               update_cap=bench.R6_HIGH_CAP)
-        assert np.array_equal(nup, ref["n_updates"]), t
-        assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), t
-        assert np.array_equal(flags, ref["flags"]), t
-        assert not (flags & 4).any()  # nothing reached the cap
-        st, ns = ref["state"], ref["n_steps"]
-    assert np.array_equal(b.get_state(), st)
+        got.append(b.env_step_multi(cfg, acts[t], update_cap=cap))
+        pools.append(b.env_grid_stats())
+    final_step = (b.get_state(), b.get_n_steps())
     b.close()
+    dev = torch.device("cuda", 0)
+    bf = G.PBNBatch(gnet, B, seed=seed, env_id_base=base)
+    bf.env_reset(cfg)
+    d_a = torch.from_numpy(acts).to(dev)
+    fo = (torch.empty((T, B, net.n_words), dtype=torch.int64, device=dev), torch.empty((T, B), dtype=torch.int32, device=dev),
+          torch.empty((T, B), dtype=torch.uint8, device=dev), torch.empty((T, B), dtype=torch.int32, device=dev))
+    bf.env_rollout_multi_device(cfg, T, d_a.data_ptr(), A, *[x.data_ptr() for x in fo], update_cap=cap)
+    bf.sync()  # raises if the pool dropped an env (sticky fault word)
+    pools.append(bf.env_grid_stats())
+    fused = [(fo[0][t].cpu().numpy().view(np.uint64), fo[1][t].cpu().numpy(), fo[2][t].cpu().numpy(),
+              fo[3][t].cpu().numpy().view(np.uint32)) for t in range(T)]
+    final_fused = (bf.get_state(), bf.get_n_steps())
+    bf.close()
+    assert all(p["gave_up"] == 0 and p["live_at_end"] == 0 for p in pools), pools
+    assert sum(p["pushed"] for p in pools[:T]) > 0 and pools[T]["pushed"] > 0, pools
+    for t in range(T):
+        ref = o.env_step_multi(cfgd, st, ns, acts[t], seed=seed, env_base=base, call_idx=t, update_cap=cap)
+        for name, g in (("per_step", got[t]), ("fused", fused[t])):
+            obs, rew, flags, nup = g
+            assert np.array_equal(nup, ref["n_updates"]), (name, t)
+            assert np.array_equal(obs, ref["obs"]) and np.array_equal(rew, ref["reward"]), (name, t)
+            assert np.array_equal(flags, ref["flags"]), (name, t)
+            assert not (flags & 4).any()  # nothing reached the cap
+        st, ns = ref["state"], ref["n_steps"]
+    for fs in (final_step, final_fused):
+        assert np.array_equal(fs[0], st) and np.array_equal(fs[1], ns)
 
 
 @pytest.mark.parametrize("steal", ["1", "0"])
@@ -345,7 +435,7 @@ def test_tail_handoff_between_waves_matches_oracle(G, oracle_mod, monkeypatch, m
     b.close()
 
 
-@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off", "grid", "grid_off", "migrate"])
+@pytest.mark.parametrize("case", ["handoff", "helpers", "helpers_off", "grid", "grid_off"])
 @pytest.mark.parametrize("mode", ["per_step", "fused"])
 def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypatch, mode, case):
     """A case in which the workgroup hand-off must happen: one workgroup (4 waves), two
@@ -365,21 +455,17 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     goes idle, so the other workgroup waits on a ticket while the loaded wave, after handing three envs
     to its idle siblings, still holds unstarted ones: it pushes envs into the pool (asserted) and the
     waiting workgroup resumes them; every output equals the oracle. ``grid_off``: PBNSIM_ENV_GRID_STEAL=0
-    (nothing pushed). ``migrate``: the same two workgroups with 4 envs -- the loaded wave hands three to its
-    siblings, so all four waves of its workgroup run long sessions with no idle wave to help them, and at a
-    16-block check a session moves itself (mid-way: used, counters, committed plane) to the waiting
-    workgroup (asserted), which resolves the rest with helpers; exact against the oracle."""
+    (nothing pushed). (Round 5's ``migrate`` case -- a running session moving itself into the pool -- went with
+    the feature: config 5's A/B showed no gain, profiles/r06_r6_pool_migrate_ab.json.)"""
     import torch
 
-    grid_case = case.startswith("grid") or case == "migrate"
+    grid_case = case.startswith("grid")
     monkeypatch.setenv("PBNSIM_ENV_LANES", "16" if grid_case else "2")
     monkeypatch.setenv("PBNSIM_ENV_GRID", "2" if grid_case else "1")
     if case == "helpers_off":
         monkeypatch.setenv("PBNSIM_ENV_HELPERS", "0")
     if case == "grid_off":
         monkeypatch.setenv("PBNSIM_ENV_GRID_STEAL", "0")
-    if case == "migrate":
-        monkeypatch.setenv("PBNSIM_ENV_MIGRATE_BLOCKS", "16")  # at the first 16-block check (default: 256)
     import sys
     from pathlib import Path
 
@@ -393,7 +479,7 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     cfgd = dict(care=cfg.cube_care, value=cfg.cube_value, target_care=cfg.target_care, target_value=cfg.target_value,
                 horizon=100)
     o = oracle_mod.Oracle(net)
-    B = {"handoff": 6, "grid": 16, "grid_off": 16, "migrate": 4}.get(case, 2)
+    B = {"handoff": 6, "grid": 16, "grid_off": 16}.get(case, 2)
     seed, base, T, A, cap = 0xAC7, 90001, 2, 4, bench.R6_HIGH_CAP
     st, ns = o.env_reset_philox(np.zeros((B, net.n_words), np.uint64), np.ones(B, np.int64), cfg.reset_care,
                                 cfg.reset_value, seed=seed, env_base=base, reset_count=0)
@@ -446,8 +532,6 @@ def test_tail_handoff_forced_happens_and_matches_oracle(G, oracle_mod, monkeypat
     assert all(p["gave_up"] == 0 and p["live_at_end"] == 0 for p in pool), pool
     if case == "grid":
         assert pool[0]["pushed"] > 0, pool  # ... and push envs to the waiting workgroup
-    if case == "migrate":
-        assert pool[0]["migrated"] > 0, pool  # ... and move a running session there
     if case == "grid_off":
         assert sum(p["pushed"] + p["tickets"] for p in pool) == 0, pool
     if case == "helpers":

@@ -28,16 +28,23 @@ def run_pass(counter: str, outdir: Path, network: str, batch: int, steps: int) -
            "--network", network, "--batch", str(batch)]
     subprocess.run(cmd, check=True, cwd=str(ROOT))
     rows = list(csv.DictReader(open(outdir / "run_counter_collection.csv")))
-    return [float(r["Counter_Value"]) for r in rows if "k_step" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    rows = [r for r in rows if "k_step" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0)))  # launch order: the window is a range of launches
+    return [float(r["Counter_Value"]) for r in rows]
+
+
+# the launches bench.py's figures are timed over (and its changed fraction q measured over): the headline's
+# --warmup 5 --steps 20 at 1M envs, beyond_mall_supplement's 50 + 200 at 8M -- so traffic and alg bytes share q
+WINDOWS = {1 << 20: (5, 20), 1 << 23: (50, 200)}
 
 
 def main():
     network = sys.argv[1] if len(sys.argv) > 1 else "bittner199"
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
-    steps = 40
+    w0, wn = WINDOWS.get(batch, (0, 40))
     base = ROOT / "gpurun_out" / "pmc"
-    fetch = run_pass("FETCH_SIZE", base / "fetch", network, batch, steps)
-    write = run_pass("WRITE_SIZE", base / "write", network, batch, steps)
+    fetch = run_pass("FETCH_SIZE", base / "fetch", network, batch, w0 + wn)[w0:w0 + wn]
+    write = run_pass("WRITE_SIZE", base / "write", network, batch, w0 + wn)[w0:w0 + wn]
     f_kib, w_kib = statistics.median(fetch), statistics.median(write)
     per_launch = f_kib * 1024 * 2 + w_kib * 1024
     out_path = ROOT / "gpurun_out" / "pmc_traffic.json"  # copied into profiles/ after review
@@ -46,6 +53,8 @@ def main():
     doc.setdefault("per_launch_bytes", {})[f"{network}:{batch}"] = per_launch
     doc.setdefault("detail", {})[f"{network}:{batch}"] = {
         "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib, "dispatches": [len(fetch), len(write)],
+        "window": [w0, w0 + wn], "FETCH_SIZE_KiB_mean": statistics.fmean(fetch),
+        "WRITE_SIZE_KiB_mean": statistics.fmean(write),
         "read_bytes_corrected": f_kib * 1024 * 2, "write_bytes": w_kib * 1024,
         "alg_bytes": 16 * ((json.loads((ROOT / "gym-pbn-stac_amd/gym_pbn_amd/data/networks.json").read_text())
                             ["networks"].get(network, {}).get("n_nodes", 199) + 63) // 64) * batch,
@@ -54,7 +63,7 @@ def main():
     tree = os.environ.get("PMC_TREE", "unknown tree")  # the commit the caller profiled (no .git on the GPU box)
     doc["detail"][f"{network}:{batch}"]["tree"] = tree
     doc["source"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on bench.py --kernel-only; "
-                     "per-launch median; FETCH_SIZE x2 (gfx950 wide-read correction), WRITE_SIZE as is; "
+                     "per-launch median over the launches bench.py times (1M: 5..25, 8M: 50..250); FETCH_SIZE x2 (gfx950 wide-read correction), WRITE_SIZE as is; "
                      f"profiled tree {tree}")
     out_path.write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps(doc["detail"][f"{network}:{batch}"]))

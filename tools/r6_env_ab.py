@@ -32,7 +32,8 @@ for rep in range(reps):
                    "per_step_M": round(d["per_step"]["env_steps_per_s"] / 1e6, 1),
                    "fused_M": round(d["fused"]["env_steps_per_s"] / 1e6, 1),
                    "helpers": [d["per_step"].get("helpers_last_launch"), d["fused"].get("helpers_last_launch")],
-                   "handoffs": [d["per_step"].get("handoffs_last_launch"), d["fused"].get("handoffs_last_launch")]}
+                   "handoffs": [d["per_step"].get("handoffs_last_launch"), d["fused"].get("handoffs_last_launch")],
+                   "pool": [d["per_step"].get("pool_last_launch"), d["fused"].get("pool_last_launch")]}
             out.append(row)
             print(json.dumps(row), flush=True)
 print(json.dumps({"B": B, "T": T, "rows": out}))

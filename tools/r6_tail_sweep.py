@@ -58,12 +58,14 @@ def child(B, T, spec, cap):
         inf = b.info()
         handoffs = b.env_handoffs()
         helpers = b.env_tail_helpers() if hasattr(b, "env_tail_helpers") else None
+        pool = b.env_grid_stats() if hasattr(b, "env_grid_stats") else None
         b.close()
         n = outs[3].to(torch.int64)
         res["fused" if fused else "per_step"] = {"ms_per_env_step": best * 1e3 / T, "env_steps_per_s": B * T / best,
                                                  "max_updates": int(n.max()), "mean_updates": float(n.float().mean()),
                                                 "env_grid": inf["env_grid"], "env_lane_limit": inf["env_lane_limit"], "env_chunk": inf.get("env_chunk"),
-                                                "handoffs_last_launch": handoffs, "helpers_last_launch": helpers}
+                                                "handoffs_last_launch": handoffs, "helpers_last_launch": helpers,
+                                                 "pool_last_launch": pool}
     print(json.dumps(res))
 
 
