@@ -10,11 +10,12 @@
 // yields the same states on the GPU as in Python, from the seed alone.
 //
 // Layout: one row of 624 u32 per env per generator, env-major ([B][MT_ROW]), plus the
-// row's read position. A lane's successive words share cache lines; the twist is run
-// by the lane itself when its position reaches 624 (sequential in-place MT19937).
+// row's read position. A lane's successive words share cache lines; a row that runs out is
+// twisted in place by the whole wave (k_mt_step below).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "pbn_device.hpp"
 #include "pbn_params.hpp"
@@ -107,7 +108,10 @@ __global__ __launch_bounds__(BLOCK) void k_mt_seed(MTArgs a) {
 // lane's result of the previous phase), coalesced: lanes reach the end of their rows at different times
 // (rejection), and the in-lane twist this replaces serialised the wave on every one of them
 // (MT mode ran at ~1 % of its memory roofline).
-constexpr uint32_t MT_CHUNK = 8;  // draws per lane per generation pass (LDS: 8 B each; 8 keeps 4 workgroups per CU)
+// draws per lane per generation pass. The draw entries are 2 B for predictor mix (round 6: the predictor choice is
+// resolved in the generation pass, MTDraw), so the buffer is 4 KiB and 6 workgroups fit a CU instead of 4:
+// 54.7 vs 50.0 G node-updates/s at 1M envs (profiles/r06_mt_mode_ab.json)
+constexpr uint32_t MT_CHUNK = 8;
 constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu, MT_A = 0x9908b0dfu;
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
@@ -181,14 +185,23 @@ struct MTWin {
     }
 };
 
-template <int W, int KIND>
+// Draw entry of the per-lane LDS buffer: truth tables keep k53 | node << 53 (the threshold row depends on the
+// state at the update); predictor mix (N <= 512, <= 128 predictors per node) resolves the predictor choice in
+// the generation pass (the thresholds depend on node and k53 only) and keeps node | choice << 9 in 16 bits --
+// a quarter of the LDS, so 6 workgroups per CU fit instead of 4 (the kernel waits on its rows' round trips)
+// (WIDE: a node with more than 128 predictors -- u32 entries, node | choice << 9)
+template <int KIND, bool WIDE>
+using MTDraw = typename std::conditional<KIND == KIND_PROB_TABLE, uint64_t,
+                                         typename std::conditional<WIDE, uint32_t, uint16_t>::type>::type;
+
+template <int W, int KIND, bool WIDE>
 __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
     extern __shared__ __align__(16) uint8_t lds[];
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
-    // per-lane draw buffer: [MT_CHUNK][BLOCK] u64 = k53 | node << 53
-    uint64_t* const dbuf = reinterpret_cast<uint64_t*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;
+    // per-lane draw buffer: [MT_CHUNK][BLOCK] entries (MTDraw)
+    MTDraw<KIND, WIDE>* const dbuf = reinterpret_cast<MTDraw<KIND, WIDE>*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;
     const uint32_t N = (uint32_t)a.L.n_nodes;
     const uint32_t lane = __lane_id();
     constexpr bool TABLE = KIND == KIND_PROB_TABLE;
@@ -234,6 +247,7 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
                     const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
                     mask &= mask - 1ull;
                     const uint64_t eL = e0 + L;
+                    // the owner's first window (new words 0..7) straight from the twist's registers: no reload
                     mt_twist_coop(a.mt_py + eL * MT_ROW, lane);
                 }
                 if constexpr (TABLE) {
@@ -273,12 +287,15 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
                         stt = 2u;
                     } else {
                         const uint64_t k53 = k53_of(wa, w);
-                        dbuf[cnt * BLOCK] = k53 | ((uint64_t)node << 53);
+                        if constexpr (TABLE)
+                            dbuf[cnt * BLOCK] = k53 | ((uint64_t)node << 53);
+                        else  // (the init draws of Bittner are single bits, stt 3 below)
+                            dbuf[cnt * BLOCK] = (MTDraw<KIND, WIDE>)(node | (predictor_choice(node, k53, lds, a.L) << 9));
                         ++cnt;
                         stt = (TABLE && a.init_state) ? 1u : 0u;
                     }
                     if (stt == 3u) {  // Bittner init bit
-                        dbuf[cnt * BLOCK] = (uint64_t)node << 53;
+                        dbuf[cnt * BLOCK] = (MTDraw<KIND, WIDE>)node;
                         ++cnt;
                         stt = 0u;
                     }
@@ -286,18 +303,26 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
             }
             // apply the chunk: every lane its cnt draws (cnt == tgt: each lane finished its chunk)
             for (uint32_t c = 0; c < tgt; ++c) {
-                const uint64_t d = dbuf[c * BLOCK];
-                const uint64_t k53 = d & ((1ull << 53) - 1ull);
-                const uint32_t r = (uint32_t)(d >> 53);
-                if (a.init_state) {
+                const MTDraw<KIND, WIDE> d = dbuf[c * BLOCK];
+                if constexpr (TABLE) {
+                    const uint64_t k53 = d & ((1ull << 53) - 1ull);
+                    const uint32_t r = (uint32_t)(d >> 53);
+                    if (a.init_state) {
+                        const uint32_t i = done + c;
+                        const uint32_t dw = i >> 5, sh = i & 31u;
+                        P.put(dw, (P.get(dw) & ~(1u << sh)) | ((k53 > (1ull << 52) ? 1u : 0u) << sh));
+                    } else {
+                        table_update_lds(P, 1u + r, k53, lds, a.L);
+                    }
+                } else if (a.init_state) {
                     const uint32_t i = done + c;
-                    const uint32_t bit = TABLE ? (k53 > (1ull << 52) ? 1u : 0u) : r;
                     const uint32_t dw = i >> 5, sh = i & 31u;
-                    P.put(dw, (P.get(dw) & ~(1u << sh)) | (bit << sh));
-                } else if constexpr (KIND == KIND_PREDICTOR_MIX) {
-                    predictor_update_lds(P, r, k53, lds, a.L);
+                    P.put(dw, (P.get(dw) & ~(1u << sh)) | ((uint32_t)d << sh));
                 } else {
-                    table_update_lds(P, 1u + r, k53, lds, a.L);
+                    const uint32_t i = (uint32_t)d & 511u, dw = i >> 5, sh = i & 31u;
+                    const uint64_t rec = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec)[i * a.L.pmax + ((uint32_t)d >> 9)];
+                    const uint32_t self = P.get(dw);
+                    P.put(dw, (self & ~(1u << sh)) | (predictor_apply(P, i, self, rec) << sh));
                 }
             }
             done += tgt;
@@ -313,20 +338,22 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
     }
 }
 
-template <int KIND>
+template <int KIND, bool WIDE>
 static void* mt_step_fn(int W) {
     switch (W) {
-        case 1: return (void*)k_mt_step<1, KIND>;
-        case 2: return (void*)k_mt_step<2, KIND>;
-        case 3: return (void*)k_mt_step<3, KIND>;
-        case 4: return (void*)k_mt_step<4, KIND>;
-        case 5: return (void*)k_mt_step<5, KIND>;
-        case 6: return (void*)k_mt_step<6, KIND>;
-        case 7: return (void*)k_mt_step<7, KIND>;
-        case 8: return (void*)k_mt_step<8, KIND>;
+        case 1: return (void*)k_mt_step<1, KIND, WIDE>;
+        case 2: return (void*)k_mt_step<2, KIND, WIDE>;
+        case 3: return (void*)k_mt_step<3, KIND, WIDE>;
+        case 4: return (void*)k_mt_step<4, KIND, WIDE>;
+        case 5: return (void*)k_mt_step<5, KIND, WIDE>;
+        case 6: return (void*)k_mt_step<6, KIND, WIDE>;
+        case 7: return (void*)k_mt_step<7, KIND, WIDE>;
+        case 8: return (void*)k_mt_step<8, KIND, WIDE>;
     }
     return nullptr;
 }
+
+static bool mt_wide(const NetLayout& L) { return L.kind == KIND_PREDICTOR_MIX && L.pmax > 128u; }
 
 int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream) {
     (void)W;
@@ -336,13 +363,18 @@ int launch_mt_seed(int W, const MTArgs& a, int grid, void* stream) {
     return (int)hipLaunchKernel(fn, dim3((unsigned)grid), dim3(BLOCK), kargs, 0, (hipStream_t)stream);
 }
 
-uint32_t mt_lds_bytes(int W, uint32_t image_bytes) { return image_bytes + 8u * (uint32_t)W * BLOCK + 8u * MT_CHUNK * BLOCK; }
+uint32_t mt_lds_bytes(int W, const NetLayout& L) {
+    const uint32_t entry = L.kind == KIND_PROB_TABLE ? 8u : mt_wide(L) ? 4u : 2u;  // MTDraw
+    return L.bytes + 8u * (uint32_t)W * BLOCK + entry * MT_CHUNK * BLOCK;
+}
 
 // grid: the resident workgroups (every wave walks 64-env tiles), capped by the tiles there are
 int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream) {
-    void* fn = a.L.kind == KIND_PREDICTOR_MIX ? mt_step_fn<KIND_PREDICTOR_MIX>(W) : mt_step_fn<KIND_PROB_TABLE>(W);
+    void* fn = a.L.kind != KIND_PREDICTOR_MIX ? mt_step_fn<KIND_PROB_TABLE, false>(W)
+               : mt_wide(a.L)                  ? mt_step_fn<KIND_PREDICTOR_MIX, true>(W)
+                                               : mt_step_fn<KIND_PREDICTOR_MIX, false>(W);
     if (!fn) return (int)hipErrorInvalidValue;
-    const uint32_t lds = mt_lds_bytes(W, a.L.bytes);
+    const uint32_t lds = mt_lds_bytes(W, a.L);
     int bpc = 0;
     if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(fn), BLOCK, lds))
         return (int)e;

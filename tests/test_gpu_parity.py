@@ -671,13 +671,15 @@ def test_mt_mode_truth_table_reproduces_reference(G, name):
 
 def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
     """65,536 envs with spread seeds (crossing many MT twists, rows running out in different iterations):
-    EVERY env vs the oracle's CPython MT (OpenMP over the envs)."""
+    EVERY env vs the oracle's CPython MT (OpenMP over the envs); T = 700 in launches of 1, 2, 97 and 600
+    updates (launches end mid-row and mid-chunk)."""
     net = load_network("bittner199")
     B, T = 65536, 700
     seeds = np.arange(B, dtype=np.uint64) * np.uint64(2654435761) + np.uint64(3)
     b = G.PBNBatch(net, B)
     b.mt_seed(seeds, init_state=True)
-    b.mt_step(T)
+    for n in (1, 2, 97, 600):
+        b.mt_step(n)
     got = b.get_state()
     b.close()
     o = oracle_mod.Oracle(net)
