@@ -48,7 +48,7 @@ def main():
     f_kib, w_kib = statistics.median(fetch), statistics.median(write)
     per_launch = f_kib * 1024 * 2 + w_kib * 1024
     out_path = ROOT / "gpurun_out" / "pmc_traffic.json"  # copied into profiles/ after review
-    prev = ROOT / "profiles" / "pmc_traffic.json"
+    prev = out_path if out_path.exists() else ROOT / "profiles" / "pmc_traffic.json"  # several sizes, one file
     doc = json.loads(prev.read_text()) if prev.exists() else {}
     doc.setdefault("per_launch_bytes", {})[f"{network}:{batch}"] = per_launch
     doc.setdefault("detail", {})[f"{network}:{batch}"] = {
