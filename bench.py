@@ -71,7 +71,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--rollout", type=int, default=64, help="updates per launch for the supplementary rollout line")
     p.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    p.add_argument("--valu-file", default=str(ROOT / "profiles" / "r05_valu_pmc.json"))
+    p.add_argument("--valu-file", default=str(ROOT / "profiles" / "r06_valu_pmc.json"))
     p.add_argument("--kernel-only", action="store_true", help="just run steps (for rocprofv3 child runs)")
     p.add_argument("--r6-chunks", type=int, default=2, help="config-5 supplement: timed T=100 chunks (0 = off)")
     p.add_argument("--r6-batch", type=int, default=131072, help="config-5 supplement: envs per GPU")
@@ -403,7 +403,7 @@ def valu_roofline(v, s, updates):
            "frac": lane_ops / s / 1e12 / VALU_PEAK_TOPS, "valu_wave_insts_per_update": ipu,
            "frac_source": "issue slots: SQ_INSTS_VALU x 64 lane-ops per wave-instruction, masked lanes included",
            "valu_busy_frac": v.get("valu_busy_frac"), "kernel_s": s, "node_updates": updates,
-           "source": v.get("source", "profiles/r05_valu_pmc.json")}
+           "source": v.get("source", "profiles/r06_valu_pmc.json")}
     alf = v.get("active_lane_frac")
     if alf is not None:  # useful work: lane-ops of enabled lanes only
         out["active_lane_frac"] = alf

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r05_valu_pmc.json (copied to
+"""VALU roofline inputs for the compute-bound kernels -> gpurun_out/r06_valu_pmc.json (copied to
 profiles/ after review; bench.py reads it for the rollout and config-5 rooflines).
 
 One rocprofv3 --pmc pass (kernel trace only; 5 SQ counters + 1 GRBM counter, within one pass's
