@@ -189,6 +189,7 @@ struct pbn_batch {
     int ssd_shared = -1;      // PBNSIM_SSD_SHARED: 0 = one wave per env, 4 / 8 = that many, 1 = the default
                               // count, -1 = by size
     int roll_group = 1;       // PBNSIM_ROLL_GROUP: lanes per env of the rollout kernel (default by size)
+    bool mt_lane_walk = false;  // PBNSIM_MT_LANES=1: MT-mode steps of predictor-mix networks on k_mt_step
     // step mode without HIP graphs: by default for large batches (a graph replay's start on the
     // device costs more than host submission, which a long kernel hides: 1M Bittner-200 envs, 20
     // launches: 9.3 us per launch plain vs 9.9 us as one replay); PBNSIM_STEP_GRAPH=0/1 forces it
@@ -559,6 +560,7 @@ int pbn_batch_create(const pbn_net* net_c, int device, uint64_t n_envs, uint64_t
     }
     b->step_graph_off = n_envs * (uint64_t)b->W >= STEP_GRAPH_MAX_WORDS;
     if (const char* v = getenv("PBNSIM_STEP_GRAPH")) b->step_graph_off = atoi(v) == 0;
+    if (const char* v = getenv("PBNSIM_MT_LANES")) b->mt_lane_walk = atoi(v) != 0;
     // rollout lanes per env: 1 = k_rollout; 2/4/8 = k_rollout_grp (predictor mix, N <= 256)
     b->roll_group = roll_group_size(b, net);
     if (const char* v = getenv("PBNSIM_ROLL_GROUP")) {
@@ -1091,6 +1093,7 @@ static MTArgs mt_args(pbn_batch* b) {
     a.mt_np = (uint32_t*)b->mt_np.p;
     a.pos_py = (uint32_t*)b->mt_pos_py.p;
     a.pos_np = (uint32_t*)b->mt_pos_np.p;
+    a.lane_walk = b->mt_lane_walk ? 1 : 0;
     return a;
 }
 

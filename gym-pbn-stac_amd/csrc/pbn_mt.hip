@@ -247,7 +247,6 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
                     const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
                     mask &= mask - 1ull;
                     const uint64_t eL = e0 + L;
-                    // the owner's first window (new words 0..7) straight from the twist's registers: no reload
                     mt_twist_coop(a.mt_py + eL * MT_ROW, lane);
                 }
                 if constexpr (TABLE) {
@@ -338,6 +337,137 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
     }
 }
 
+// ---- MT mode, predictor-mix steps (Bittner Graph.step; round 6): the per-lane walk with staged windows.
+// k_mt_step reads each lane's row 16 B at a time as it walks, and since any lane may move to its next 16 B in any
+// iteration, its loop waits for all its loads (s_waitcnt vmcnt(0)) every iteration: a memory round trip per word
+// (the SQ counters: 75 % of its cycles waiting, profiles/r06_mt_lanes_sq_pmc.csv). Here a lane's next MT_WIN words
+// (from pos rounded down to 16 B) are brought into the wave's LDS by asynchronous LDS-DMA loads (global_load_lds,
+// 16 B per lane per instruction, no VGPRs), ONE wait for the whole window, and the walk then reads its words from
+// LDS, each one prefetched an iteration ahead; a lane whose window runs out before its chunk's draws are made takes
+// the next window in the next pass; the machine runs as selects. Same draws, same state machine, same entries, same
+// rows and positions as k_mt_step (bit-exact; the tests run both walks). Bench workload (1M envs, T = 256): 62.4 G
+// node-updates/s vs 54.8 (k_mt_step, u16 entries) and 50.0 (round 5); windows of 8 / 16 / 32 words gave 60.3 / 50.9
+// / 40.1 G (fewer workgroups per CU as the windows grow), so 12 (profiles/r06_mt_mode_ab.json).
+#ifndef PBN_MT_WIN
+#define PBN_MT_WIN 12
+#endif
+constexpr uint32_t MT_WIN = PBN_MT_WIN;  // words per staged window: MT_WIN / 4 DMA loads per lane
+static_assert(MT_WIN % 4u == 0 && MT_WIN >= 8u, "windows of 16-B granules");
+
+template <int W, bool WIDE>
+__global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
+    using D = MTDraw<KIND_PREDICTOR_MIX, WIDE>;
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    typedef __attribute__((address_space(3))) uint32_t l32;
+    extern __shared__ __align__(16) uint8_t lds[];
+    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    __syncthreads();
+    const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
+    D* const dbuf = reinterpret_cast<D*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;  // [MT_CHUNK][BLOCK]
+    // the wave's windows: granule j (16 B) of lane l at j * 1 KiB + l * 16
+    uint8_t* const win = lds + a.L.bytes + 8u * W * BLOCK + (uint32_t)sizeof(D) * MT_CHUNK * BLOCK + (threadIdx.x >> 6) * (MT_WIN * 256u);
+    const uint32_t lane = __lane_id();
+    const uint32_t* const mine = reinterpret_cast<const uint32_t*>(win + lane * 16u);
+    auto word = [&](uint32_t k) { return mine[(k >> 2) * 256u + (k & 3u)]; };  // window word k (< MT_WIN)
+    const uint64_t* const recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+    const uint32_t N = (uint32_t)a.L.n_nodes;
+    const uint32_t ks = (uint32_t)__clz(N);  // randint(0, N - 1): _randbelow(N), getrandbits(bit_length(N)) < N
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t e0 = (uint64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63u); e0 < a.B; e0 += stride) {
+        const uint64_t e = e0 + lane;
+        const bool valid = e < a.B;
+        uint32_t* const row = a.mt_py + (valid ? e : e0) * MT_ROW;  // lanes past B stage lane 0's row (unused)
+        uint64_t st[W];
+        if (valid) {
+            load_state<W>(a.state + e * W, st);
+        } else {
+#pragma unroll
+            for (int k = 0; k < W; ++k) st[k] = 0;
+        }
+        to_plane<W>(P, st);
+        uint32_t pos = valid ? a.pos_py[e] : 0u, left = valid ? a.T : 0u;
+        uint32_t stt = 0, node = 0, wa = 0;  // machine: 0 node word (rejection), 1 random()'s first word, 2 its second
+        while (__ballot(left > 0u) != 0ull) {
+            const uint32_t tgt = min(left, MT_CHUNK);
+            uint32_t cnt = 0;
+            for (;;) {
+                bool want = cnt < tgt;
+                if (__ballot(want) == 0ull) break;
+                uint64_t mask = __ballot(want && pos >= MT_N);
+                if (mask) {
+                    while (mask) {  // rows that have run out: twisted by the whole wave (k_mt_step)
+                        const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                        mask &= mask - 1ull;
+                        mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (want && pos >= MT_N) pos = 0;
+                }
+                // stage words [base, base + MT_WIN) of every lane's row, base = pos rounded down to 16 B; granules
+                // past the row's end repeat its last one (never read: a lane stops at the row's end). The window's
+                // previous reads are done first (an LDS-DMA write does not wait for them). (Handing a twisted row's
+                // first words to its owner through LDS instead of staging them: no gain, 62.1 vs 62.2 G.)
+                const uint32_t base = pos & ~3u;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
+                    __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u), 16,
+                                                     0, 0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t end = min(base + MT_WIN, MT_N);
+                uint32_t wn = word(min(pos - base, MT_WIN - 1u));  // the next word, read an iteration ahead
+                while (__ballot(want && pos < end) != 0ull) {
+                    // the machine as selects (one divergent branch, the draw's store, instead of three)
+                    const bool act = want && pos < end;
+                    const uint32_t w = mt_temper(wn);
+                    pos += act ? 1u : 0u;
+                    wn = word(min(pos - base, MT_WIN - 1u));
+                    const uint32_t r = w >> ks;  // _randbelow: rejected if >= N
+                    const bool take_node = act && stt == 0u && r < N, take_wa = act && stt == 1u, emit = act && stt == 2u;
+                    const uint32_t ent = node | (predictor_choice(node, k53_of(wa, w), lds, a.L) << 9);
+                    if (emit) dbuf[cnt * BLOCK] = (D)ent;
+                    node = take_node ? r : node;
+                    wa = take_wa ? w : wa;
+                    stt = take_node ? 1u : take_wa ? 2u : emit ? 0u : stt;
+                    cnt += emit ? 1u : 0u;
+                    want = cnt < tgt;
+                }
+            }
+            // apply the chunk: every lane its tgt draws
+            for (uint32_t c = 0; c < tgt; ++c) {
+                const uint32_t d = dbuf[c * BLOCK];
+                const uint32_t i = d & 511u, dw = i >> 5, sh = i & 31u;
+                const uint64_t rec = recs[i * a.L.pmax + (d >> 9)];
+                const uint32_t self = P.get(dw);
+                P.put(dw, (self & ~(1u << sh)) | (predictor_apply(P, i, self, rec) << sh));
+            }
+            left -= tgt;
+        }
+        if (valid) {
+            from_plane<W>(P, st);
+            store_state<W>(a.state + e * W, st);
+            a.pos_py[e] = pos;
+        }
+    }
+}
+
+template <bool WIDE>
+static void* mt_staged_fn(int W) {
+    switch (W) {
+        case 1: return (void*)k_mt_staged<1, WIDE>;
+        case 2: return (void*)k_mt_staged<2, WIDE>;
+        case 3: return (void*)k_mt_staged<3, WIDE>;
+        case 4: return (void*)k_mt_staged<4, WIDE>;
+        case 5: return (void*)k_mt_staged<5, WIDE>;
+        case 6: return (void*)k_mt_staged<6, WIDE>;
+        case 7: return (void*)k_mt_staged<7, WIDE>;
+        case 8: return (void*)k_mt_staged<8, WIDE>;
+    }
+    return nullptr;
+}
+
 template <int KIND, bool WIDE>
 static void* mt_step_fn(int W) {
     switch (W) {
@@ -370,11 +500,14 @@ uint32_t mt_lds_bytes(int W, const NetLayout& L) {
 
 // grid: the resident workgroups (every wave walks 64-env tiles), capped by the tiles there are
 int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream) {
-    void* fn = a.L.kind != KIND_PREDICTOR_MIX ? mt_step_fn<KIND_PROB_TABLE, false>(W)
+    // predictor-mix steps: the staged walk (genRandState's init draws and truth tables: k_mt_step)
+    const bool staged = a.L.kind == KIND_PREDICTOR_MIX && !a.init_state && !a.lane_walk;
+    void* fn = staged                            ? (mt_wide(a.L) ? mt_staged_fn<true>(W) : mt_staged_fn<false>(W))
+               : a.L.kind != KIND_PREDICTOR_MIX ? mt_step_fn<KIND_PROB_TABLE, false>(W)
                : mt_wide(a.L)                  ? mt_step_fn<KIND_PREDICTOR_MIX, true>(W)
                                                : mt_step_fn<KIND_PREDICTOR_MIX, false>(W);
     if (!fn) return (int)hipErrorInvalidValue;
-    const uint32_t lds = mt_lds_bytes(W, a.L);
+    const uint32_t lds = mt_lds_bytes(W, a.L) + (staged ? MT_WIN * 4u * BLOCK : 0u);
     int bpc = 0;
     if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(fn), BLOCK, lds))
         return (int)e;

@@ -182,6 +182,7 @@ struct MTArgs {
     uint32_t* mt_np;        // [B][MT_ROW] numpy legacy RandomState (probability-table networks)
     uint32_t* pos_py;       // [B] next word index (624 = twist before next use: k_mt_step twists it, coalesced)
     uint32_t* pos_np;
+    int32_t lane_walk;      // predictor-mix steps on k_mt_step instead of k_mt_staged (PBNSIM_MT_LANES=1, tests)
 };
 
 constexpr int SSD_DAG_KMAX = 6;

@@ -145,7 +145,8 @@ int pbn_net_select_u32(const pbn_net *net, int32_t node, uint32_t a, uint64_t *r
  * PBNSIM_ENV_LANES, PBNSIM_ENV_STEAL, PBNSIM_ENV_HELPERS, PBNSIM_ENV_GRID_STEAL, PBNSIM_ENV_KERNEL_IMAGE (R6 env kernel);
  * every one is set by a `-m gpu` test; A/B-only knobs are compiled in by -DPBN_MEASURE_KNOBS (tools/build_exp.sh);
  * PBNSIM_SSD_WAVE, PBNSIM_SSD_SERIAL, PBNSIM_SSD_SHARED (SSD); PBNSIM_ROLL_GROUP (rollout lanes per env);
- * PBNSIM_STEP_GRAPH=0 (pbn_step without HIP graphs). */
+ * PBNSIM_STEP_GRAPH=0 (pbn_step without HIP graphs); PBNSIM_MT_LANES=1 (MT-mode steps of predictor-mix networks
+ * on k_mt_step's per-lane loads instead of k_mt_staged's LDS windows). */
 int pbn_batch_create(const pbn_net *net, int device, uint64_t n_envs, uint64_t env_id_base, uint64_t seed,
                      pbn_batch **out);
 void pbn_batch_destroy(pbn_batch *b);

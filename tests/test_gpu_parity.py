@@ -641,9 +641,13 @@ def test_vec_env_and_single_env_adapters(G):
 
 
 # ----------------------------------------------------------------- MT mode: reference streams on device
+@pytest.mark.parametrize("walk", ["staged", "lanes"])
 @pytest.mark.parametrize("name", ["bittner28", "bittner199"])
-def test_mt_mode_reproduces_reference_from_seed(G, name):
-    """random.seed(s); genRandState(); T x Graph.step() -- reproduced on the GPU from s alone."""
+def test_mt_mode_reproduces_reference_from_seed(G, monkeypatch, name, walk):
+    """random.seed(s); genRandState(); T x Graph.step() -- reproduced on the GPU from s alone, by the walk with
+    LDS-staged windows (k_mt_staged, the default for these networks) and the per-lane loads (k_mt_step,
+    PBNSIM_MT_LANES=1)."""
+    monkeypatch.setenv("PBNSIM_MT_LANES", "1" if walk == "lanes" else "0")
     z = golden(f"r1_mt_{name}.npz")
     b = G.PBNBatch(name, len(z["seeds"]))
     b.mt_seed(z["seeds"], init_state=True)
@@ -669,10 +673,12 @@ def test_mt_mode_truth_table_reproduces_reference(G, name):
     assert np.array_equal(b.get_state(), z["states"][:, -1])
 
 
-def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
+@pytest.mark.parametrize("walk", ["staged", "lanes"])
+def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod, monkeypatch, walk):
     """65,536 envs with spread seeds (crossing many MT twists, rows running out in different iterations):
-    EVERY env vs the oracle's CPython MT (OpenMP over the envs); T = 700 in launches of 1, 2, 97 and 600
-    updates (launches end mid-row and mid-chunk)."""
+    EVERY env vs the oracle's CPython MT (OpenMP over the envs), both walks; T = 700 in launches of 1, 2, 97
+    and 600 updates (launches end mid-row, mid-window and mid-chunk)."""
+    monkeypatch.setenv("PBNSIM_MT_LANES", "1" if walk == "lanes" else "0")
     net = load_network("bittner199")
     B, T = 65536, 700
     seeds = np.arange(B, dtype=np.uint64) * np.uint64(2654435761) + np.uint64(3)
@@ -688,10 +694,12 @@ def test_mt_mode_many_seeds_vs_oracle(G, oracle_mod):
         G.PBNBatch("tt8", 2).mt_seed(np.array([1, 2**33], dtype=np.uint64))
 
 
-def test_mt_mode_bench_workload_vs_oracle(G, oracle_mod):
+@pytest.mark.parametrize("walk", ["staged", "lanes"])
+def test_mt_mode_bench_workload_vs_oracle(G, oracle_mod, monkeypatch, walk):
     """bench.py's MT workload itself (mt_supplement: Bittner-199, 1,048,576 envs seeded 12345 + id, the
     state from genRandState, T = 256 updates per pbn_mt_step launch): two launches, every env vs the oracle's
-    run_mt from the seeds alone (16 threads)."""
+    run_mt from the seeds alone (16 threads); both walks."""
+    monkeypatch.setenv("PBNSIM_MT_LANES", "1" if walk == "lanes" else "0")
     net = load_network("bittner199")
     B, T = 1 << 20, 256
     seeds = np.arange(B, dtype=np.uint64) + np.uint64(12345)
