@@ -119,8 +119,8 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
     return m ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
 }
 
-// Twist one row in place, all 64 lanes of the wave active (row: wave-uniform).
-__device__ __forceinline__ void mt_twist_coop(uint32_t* __restrict__ row, uint32_t lane) {
+// Twist one row in place, all 64 lanes of the wave active (row: wave-uniform). Returns new word `lane` of the row.
+__device__ __forceinline__ uint32_t mt_twist_coop(uint32_t* __restrict__ row, uint32_t lane) {
     uint32_t o1[4], p1[4], m1[4], o2[4], p2[4], o3[3], p3[3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -161,6 +161,7 @@ __device__ __forceinline__ void mt_twist_coop(uint32_t* __restrict__ row, uint32
         // k3 = 623 (lane 41, j = 2): mt[623] = mt[396] ^ f(mt[623], mt[0]) with mt[0], mt[396] already new
         if (k3 < 624u) row[k3] = mt_mix(o3[j], k3 == 623u ? new0 : p3[j], n2[j]);
     }
+    return n1[0];
 }
 
 // One MT stream of one lane: row, next word index (624: twist first), 4-word window + prefetch
@@ -393,29 +394,32 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
             for (;;) {
                 bool want = cnt < tgt;
                 if (__ballot(want) == 0ull) break;
-                uint64_t mask = __ballot(want && pos >= MT_N);
-                if (mask) {
-                    while (mask) {  // rows that have run out: twisted by the whole wave (k_mt_step)
-                        const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-                        mask &= mask - 1ull;
-                        mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (want && pos >= MT_N) pos = 0;
-                }
                 // stage words [base, base + MT_WIN) of every lane's row, base = pos rounded down to 16 B; granules
                 // past the row's end repeat its last one (never read: a lane stops at the row's end). The window's
-                // previous reads are done first (an LDS-DMA write does not wait for them). (Handing a twisted row's
-                // first words to its owner through LDS instead of staging them: no gain, 62.1 vs 62.2 G.)
+                // previous reads are done first (an LDS-DMA write does not wait for them). A row that has run out
+                // is twisted by the whole wave while the other lanes' windows are in flight, and its first MT_WIN
+                // new words go to its owner's window from the twisting lanes' registers.
+                const bool tw = want && pos >= MT_N;
+                uint64_t mask = __ballot(tw);
+                if (tw) pos = 0;
                 const uint32_t base = pos & ~3u;
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (!tw) {
 #pragma unroll
-                for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
-                    __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u), 16,
-                                                     0, 0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
+                        __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u),
+                                                         16, 0, 0);
+                }
+                while (mask) {
+                    const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                    mask &= mask - 1ull;
+                    const uint32_t nw = mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
+                    if (lane < MT_WIN) *reinterpret_cast<uint32_t*>(win + (lane >> 2) * 1024u + L * 16u + (lane & 3u) * 4u) = nw;
+                    // the row's later windows are staged from what the other lanes wrote (k_mt_step's fence)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 const uint32_t end = min(base + MT_WIN, MT_N);
                 uint32_t wn = word(min(pos - base, MT_WIN - 1u));  // the next word, read an iteration ahead
                 while (__ballot(want && pos < end) != 0ull) {
