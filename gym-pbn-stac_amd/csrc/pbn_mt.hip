@@ -122,21 +122,22 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
 // Twist one row in place, all 64 lanes of the wave active (row: wave-uniform). Returns new word `lane` of the row.
 __device__ __forceinline__ uint32_t mt_twist_coop(uint32_t* __restrict__ row, uint32_t lane) {
     uint32_t o1[4], p1[4], m1[4], o2[4], p2[4], o3[3], p3[3];
+    // every load unconditional (indices clamped into the row; the clamped lanes' words are never stored), so all
+    // 26 are in flight together: conditional loads became a branch and a round trip each
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const uint32_t k1 = lane + 64u * j, k2 = 227u + lane + 64u * j;
-        const bool v1 = k1 < 227u;
-        o1[j] = v1 ? row[k1] : 0u;
-        p1[j] = v1 ? row[k1 + 1u] : 0u;
-        m1[j] = v1 ? row[k1 + 397u] : 0u;
-        o2[j] = v1 ? row[k2] : 0u;  // k2 < 454 exactly when k1 < 227
-        p2[j] = v1 ? row[k2 + 1u] : 0u;
+        const uint32_t k1 = min(lane + 64u * j, 226u), k2 = 227u + k1;
+        o1[j] = row[k1];
+        p1[j] = row[k1 + 1u];
+        m1[j] = row[k1 + 397u];
+        o2[j] = row[k2];
+        p2[j] = row[k2 + 1u];
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const uint32_t k3 = 454u + lane + 64u * j;
-        o3[j] = k3 < 624u ? row[k3] : 0u;
-        p3[j] = k3 < 623u ? row[k3 + 1u] : 0u;
+        const uint32_t k3 = min(454u + lane + 64u * j, 623u);
+        o3[j] = row[k3];
+        p3[j] = row[min(k3 + 1u, 623u)];
     }
     // every old word is read before any new word is written (other lanes read what this lane overwrites)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
