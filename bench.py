@@ -341,9 +341,11 @@ def mt_supplement(net, device, B=1 << 20, T=256, reps=3):
     """MT mode: every env runs the reference's own CPython MT19937, seeded from the
     Python seed alone (random.seed(s); genRandState(); Graph.step() x T, base.py:7,94,306-312,368-370) --
     the path that reproduces the reference bit for bit from its seed. Bittner-199, 1,048,576 envs, T updates
-    per pbn_mt_step launch. Algorithmic bytes: the MT words an update consumes (MT_WORDS_PER_UPDATE) each
-    twisted once (read + written, 8 B per word: the 2,496-B table per 624 words) + the packed state read and
-    written once per launch; against the 8 TB/s HBM spec (the 2.5 GiB of tables are past the MALL)."""
+    per pbn_mt_step launch. Algorithmic bytes: the MT words an update consumes (MT_WORDS_PER_UPDATE), each
+    twisted once (read + written) and read once by the walk that draws from it (12 B per word: the 2,496-B
+    table per 624 words three times; the walk comes hundreds of updates after the twist, so the word is
+    re-read, not kept) + the packed state read and written once per launch; against the 8 TB/s HBM spec (the
+    2.5 GiB of tables are past the MALL)."""
     import numpy as np
 
     from gym_pbn_amd.batch import PBNBatch
@@ -359,14 +361,15 @@ def mt_supplement(net, device, B=1 << 20, T=256, reps=3):
     ms, n = b.timing_read()
     b.close()
     s = ms / 1e3 / reps
-    alg = B * T * MT_WORDS_PER_UPDATE * 8 + 16 * net.n_words * B
+    alg = B * T * MT_WORDS_PER_UPDATE * 12 + 16 * net.n_words * B
     return {"workload": f"MT mode (reference RNG streams on the device), Bittner-199, {B} envs, T = {T} updates "
                         "per launch", "node_updates_per_s": B * T / s, "ms_per_launch": s * 1e3,
             "roofline": {"bound": "hbm", "achieved": alg / s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / s / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "alg_bytes_rule": f"{MT_WORDS_PER_UPDATE:.3f} MT words per update x 8 B (twist read + write) "
+                         "alg_bytes_rule": f"{MT_WORDS_PER_UPDATE:.3f} MT words per update x 12 B (twist read + write, walk "
+                              "read) "
                                            "+ 16W B of packed state per env per launch"},
-            "kernel": "pbn::k_mt_step (draw generation pass + cooperative twists, csrc/pbn_mt.hip)"}
+            "kernel": "pbn::k_mt_staged (LDS-DMA windows, draw ring, cooperative twists; csrc/pbn_mt.hip)"}
 
 
 def rollout_supplement(net, B, device, seed, T, valu):

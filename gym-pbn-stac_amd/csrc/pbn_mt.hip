@@ -345,18 +345,36 @@ __global__ __launch_bounds__(BLOCK) void k_mt_step(MTArgs a) {
 // (the SQ counters: 75 % of its cycles waiting, profiles/r06_mt_lanes_sq_pmc.csv). Here a lane's next MT_WIN words
 // (from pos rounded down to 16 B) are brought into the wave's LDS by asynchronous LDS-DMA loads (global_load_lds,
 // 16 B per lane per instruction, no VGPRs), ONE wait for the whole window, and the walk then reads its words from
-// LDS, each one prefetched an iteration ahead; a lane whose window runs out before its chunk's draws are made takes
-// the next window in the next pass; the machine runs as selects. Same draws, same state machine, same entries, same
-// rows and positions as k_mt_step (bit-exact; the tests run both walks). Bench workload (1M envs, T = 256): 62.4 G
-// node-updates/s vs 54.8 (k_mt_step, u16 entries) and 50.0 (round 5); windows of 8 / 16 / 32 words gave 60.3 / 50.9
-// / 40.1 G (fewer workgroups per CU as the windows grow), so 12 (profiles/r06_mt_mode_ab.json).
+// LDS, each one prefetched an iteration ahead; a lane whose window runs out takes the next window in the next pass.
+// Windows outlive the apply phases (restaging at every phase cost a round trip each). The draws wait in a per-lane ring
+// of MT_RING entries and a phase applies MT_APPLY per lane: a lane that has its draws keeps walking until its ring
+// is full instead of idling while the wave's slowest lane catches up (a draw takes 2 + a variable number of node
+// words: rejection). The twist's 26 loads are all in flight at once; a run-out row is twisted while the other lanes'
+// windows are in flight and its first words go to its owner's window from registers. The machine runs as selects.
+// Same draws, same state machine, same entries, same rows and positions as k_mt_step (bit-exact; the tests run both
+// walks). Bench workload (1M envs, T = 256): 89 G node-updates/s vs 54.8 (k_mt_step) and 50.0 (round 5); the steps
+// are in profiles/r06_mt_mode_ab.json.
 #ifndef PBN_MT_WIN
-#define PBN_MT_WIN 12
+#define PBN_MT_WIN 16  // 12 / 16 / 20: 86.5 / 89.2 / 87.6 G (3 workgroups per CU for all three)
 #endif
 constexpr uint32_t MT_WIN = PBN_MT_WIN;  // words per staged window: MT_WIN / 4 DMA loads per lane
 static_assert(MT_WIN % 4u == 0 && MT_WIN >= 8u, "windows of 16-B granules");
+#ifndef PBN_MT_APPLY
+#define PBN_MT_APPLY 8
+#endif
+// draws applied per lane per phase; a lane that has them keeps walking until its ring (MT_RING) is full instead of
+// idling while the wave's slowest lane catches up (a draw takes a variable number of words: rejection)
+constexpr uint32_t MT_APPLY = PBN_MT_APPLY;
+#ifndef PBN_MT_RING
+#define PBN_MT_RING 16  // ring / apply 8 / 8: 78.6 G, 16 / 8: 85.8, 16 / 4: 84.7, 16 / 12: 82.4, 32 / 16: 85.6 (W 12)
+#endif
+constexpr uint32_t MT_RING = PBN_MT_RING;  // draw entries per lane in the ring
+static_assert(MT_APPLY >= 1u && MT_APPLY <= MT_RING && MT_RING >= MT_CHUNK && (MT_RING & (MT_RING - 1u)) == 0u,
+              "ring of a power of two");
 
-template <int W, bool WIDE>
+// TP4: every node's thresholds padded to 4 (Bittner-199), read an iteration ahead (loop-carried) so that their LDS
+// round trip overlaps the next iteration's temper
+template <int W, bool WIDE, bool TP4>
 __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     using D = MTDraw<KIND_PREDICTOR_MIX, WIDE>;
     typedef __attribute__((address_space(1))) uint32_t g32;
@@ -365,13 +383,14 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
     __syncthreads();
     const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
-    D* const dbuf = reinterpret_cast<D*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;  // [MT_CHUNK][BLOCK]
+    D* const dbuf = reinterpret_cast<D*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;  // [MT_RING][BLOCK]
     // the wave's windows: granule j (16 B) of lane l at j * 1 KiB + l * 16
-    uint8_t* const win = lds + a.L.bytes + 8u * W * BLOCK + (uint32_t)sizeof(D) * MT_CHUNK * BLOCK + (threadIdx.x >> 6) * (MT_WIN * 256u);
+    uint8_t* const win = lds + a.L.bytes + 8u * W * BLOCK + (uint32_t)sizeof(D) * MT_RING * BLOCK + (threadIdx.x >> 6) * (MT_WIN * 256u);
     const uint32_t lane = __lane_id();
     const uint32_t* const mine = reinterpret_cast<const uint32_t*>(win + lane * 16u);
     auto word = [&](uint32_t k) { return mine[(k >> 2) * 256u + (k & 3u)]; };  // window word k (< MT_WIN)
     const uint64_t* const recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
+    const ulonglong2* const thr4 = reinterpret_cast<const ulonglong2*>(lds + a.L.off_thr);
     const uint32_t N = (uint32_t)a.L.n_nodes;
     const uint32_t ks = (uint32_t)__clz(N);  // randint(0, N - 1): _randbelow(N), getrandbits(bit_length(N)) < N
     const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
@@ -389,65 +408,95 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
         to_plane<W>(P, st);
         uint32_t pos = valid ? a.pos_py[e] : 0u, left = valid ? a.T : 0u;
         uint32_t stt = 0, node = 0, wa = 0;  // machine: 0 node word (rejection), 1 random()'s first word, 2 its second
+        // the draws wait in a per-lane ring of MT_RING entries: `pend` made and not yet applied, the next one written
+        // to slot `wr`; every phase applies MT_APPLY per lane, oldest first (slot `rd`, the same in every lane)
+        uint32_t pend = 0, wr = 0, rd = 0;
+        uint32_t base = pos & ~3u, end = 0;  // the lane's window [base, end) of its row; none staged yet
         while (__ballot(left > 0u) != 0ull) {
-            const uint32_t tgt = min(left, MT_CHUNK);
-            uint32_t cnt = 0;
+            const uint32_t tgt = min(left, MT_APPLY);
+            const uint32_t cap = min(left, MT_RING);  // never a draw past this launch's T
             for (;;) {
-                bool want = cnt < tgt;
-                if (__ballot(want) == 0ull) break;
-                // stage words [base, base + MT_WIN) of every lane's row, base = pos rounded down to 16 B; granules
-                // past the row's end repeat its last one (never read: a lane stops at the row's end). The window's
-                // previous reads are done first (an LDS-DMA write does not wait for them). A row that has run out
-                // is twisted by the whole wave while the other lanes' windows are in flight, and its first MT_WIN
-                // new words go to its owner's window from the twisting lanes' registers.
-                const bool tw = want && pos >= MT_N;
-                uint64_t mask = __ballot(tw);
-                if (tw) pos = 0;
-                const uint32_t base = pos & ~3u;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (!tw) {
+                bool need = pend < tgt;
+                if (__ballot(need) == 0ull) break;
+                bool can = pend < cap;
+                // a new window only when no lane that needs draws has words left in its window (windows outlive the
+                // phases: restaging at every phase cost a round trip per phase)
+                if (__ballot(need && pos < end) == 0ull) {
+                    // stage words [base, base + MT_WIN) of every lane's row, base = pos rounded down to 16 B; granules
+                    // past the row's end repeat its last one (never read: a lane stops at the row's end). The window's
+                    // previous reads are done first (an LDS-DMA write does not wait for them). A row that has run out
+                    // is twisted by the whole wave while the other lanes' windows are in flight, and its first MT_WIN
+                    // new words go to its owner's window from the twisting lanes' registers.
+                    const bool tw = need && pos >= MT_N;
+                    uint64_t mask = __ballot(tw);
+                    if (tw) pos = 0;
+                    base = pos & ~3u;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (!tw) {
 #pragma unroll
-                    for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
-                        __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u),
-                                                         16, 0, 0);
+                        for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
+                            __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u),
+                                                             16, 0, 0);
+                    }
+                    while (mask) {
+                        const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                        mask &= mask - 1ull;
+                        const uint32_t nw = mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
+                        if (lane < MT_WIN) *reinterpret_cast<uint32_t*>(win + (lane >> 2) * 1024u + L * 16u + (lane & 3u) * 4u) = nw;
+                        // the row's later windows are staged from what the other lanes wrote (k_mt_step's fence)
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    }
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                    end = min(base + MT_WIN, MT_N);
                 }
-                while (mask) {
-                    const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-                    mask &= mask - 1ull;
-                    const uint32_t nw = mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
-                    if (lane < MT_WIN) *reinterpret_cast<uint32_t*>(win + (lane >> 2) * 1024u + L * 16u + (lane & 3u) * 4u) = nw;
-                    // the row's later windows are staged from what the other lanes wrote (k_mt_step's fence)
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                const uint32_t end = min(base + MT_WIN, MT_N);
                 uint32_t wn = word(min(pos - base, MT_WIN - 1u));  // the next word, read an iteration ahead
-                while (__ballot(want && pos < end) != 0ull) {
+                ulonglong2 t0{}, t1{};
+                if constexpr (TP4) {
+                    t0 = thr4[2u * node];
+                    t1 = thr4[2u * node + 1u];
+                }
+                // walk while a lane that needs draws has words; a lane with room in its ring walks along
+                while (__ballot(need && pos < end) != 0ull) {
                     // the machine as selects (one divergent branch, the draw's store, instead of three)
-                    const bool act = want && pos < end;
+                    const bool act = can && pos < end;
                     const uint32_t w = mt_temper(wn);
                     pos += act ? 1u : 0u;
                     wn = word(min(pos - base, MT_WIN - 1u));
                     const uint32_t r = w >> ks;  // _randbelow: rejected if >= N
                     const bool take_node = act && stt == 0u && r < N, take_wa = act && stt == 1u, emit = act && stt == 2u;
-                    const uint32_t ent = node | (predictor_choice(node, k53_of(wa, w), lds, a.L) << 9);
-                    if (emit) dbuf[cnt * BLOCK] = (D)ent;
+                    const uint64_t k53 = k53_of(wa, w);
+                    uint32_t choice;
+                    if constexpr (TP4)
+                        choice = (k53 >= t0.x ? 1u : 0u) + (k53 >= t0.y ? 1u : 0u) + (k53 >= t1.x ? 1u : 0u) +
+                                 (k53 >= t1.y ? 1u : 0u);
+                    else
+                        choice = predictor_choice(node, k53, lds, a.L);
+                    const uint32_t ent = node | (choice << 9);
+                    if (emit) dbuf[wr * BLOCK] = (D)ent;
                     node = take_node ? r : node;
                     wa = take_wa ? w : wa;
                     stt = take_node ? 1u : take_wa ? 2u : emit ? 0u : stt;
-                    cnt += emit ? 1u : 0u;
-                    want = cnt < tgt;
+                    pend += emit ? 1u : 0u;
+                    wr = (wr + (emit ? 1u : 0u)) & (MT_RING - 1u);
+                    need = pend < tgt;
+                    can = pend < cap;
+                    if constexpr (TP4) {  // the next iteration's thresholds, read an iteration ahead like its word
+                        t0 = thr4[2u * node];
+                        t1 = thr4[2u * node + 1u];
+                    }
                 }
             }
-            // apply the chunk: every lane its tgt draws
+            // apply the phase: every lane its tgt oldest draws
             for (uint32_t c = 0; c < tgt; ++c) {
-                const uint32_t d = dbuf[c * BLOCK];
+                const uint32_t d = dbuf[((rd + c) & (MT_RING - 1u)) * BLOCK];
                 const uint32_t i = d & 511u, dw = i >> 5, sh = i & 31u;
                 const uint64_t rec = recs[i * a.L.pmax + (d >> 9)];
                 const uint32_t self = P.get(dw);
                 P.put(dw, (self & ~(1u << sh)) | (predictor_apply(P, i, self, rec) << sh));
             }
+            rd = (rd + tgt) & (MT_RING - 1u);
+            pend -= tgt;
             left -= tgt;
         }
         if (valid) {
@@ -458,17 +507,17 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     }
 }
 
-template <bool WIDE>
+template <bool WIDE, bool TP4>
 static void* mt_staged_fn(int W) {
     switch (W) {
-        case 1: return (void*)k_mt_staged<1, WIDE>;
-        case 2: return (void*)k_mt_staged<2, WIDE>;
-        case 3: return (void*)k_mt_staged<3, WIDE>;
-        case 4: return (void*)k_mt_staged<4, WIDE>;
-        case 5: return (void*)k_mt_staged<5, WIDE>;
-        case 6: return (void*)k_mt_staged<6, WIDE>;
-        case 7: return (void*)k_mt_staged<7, WIDE>;
-        case 8: return (void*)k_mt_staged<8, WIDE>;
+        case 1: return (void*)k_mt_staged<1, WIDE, TP4>;
+        case 2: return (void*)k_mt_staged<2, WIDE, TP4>;
+        case 3: return (void*)k_mt_staged<3, WIDE, TP4>;
+        case 4: return (void*)k_mt_staged<4, WIDE, TP4>;
+        case 5: return (void*)k_mt_staged<5, WIDE, TP4>;
+        case 6: return (void*)k_mt_staged<6, WIDE, TP4>;
+        case 7: return (void*)k_mt_staged<7, WIDE, TP4>;
+        case 8: return (void*)k_mt_staged<8, WIDE, TP4>;
     }
     return nullptr;
 }
@@ -507,12 +556,15 @@ uint32_t mt_lds_bytes(int W, const NetLayout& L) {
 int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream) {
     // predictor-mix steps: the staged walk (genRandState's init draws and truth tables: k_mt_step)
     const bool staged = a.L.kind == KIND_PREDICTOR_MIX && !a.init_state && !a.lane_walk;
-    void* fn = staged                            ? (mt_wide(a.L) ? mt_staged_fn<true>(W) : mt_staged_fn<false>(W))
+    const bool tp4 = a.L.tp == 4u;
+    void* fn = staged ? (mt_wide(a.L) ? (tp4 ? mt_staged_fn<true, true>(W) : mt_staged_fn<true, false>(W))
+                                      : (tp4 ? mt_staged_fn<false, true>(W) : mt_staged_fn<false, false>(W)))
                : a.L.kind != KIND_PREDICTOR_MIX ? mt_step_fn<KIND_PROB_TABLE, false>(W)
                : mt_wide(a.L)                  ? mt_step_fn<KIND_PREDICTOR_MIX, true>(W)
                                                : mt_step_fn<KIND_PREDICTOR_MIX, false>(W);
     if (!fn) return (int)hipErrorInvalidValue;
-    const uint32_t lds = mt_lds_bytes(W, a.L) + (staged ? MT_WIN * 4u * BLOCK : 0u);
+    const uint32_t entry = mt_wide(a.L) ? 4u : 2u;  // staged: MT_WIN-word windows, a ring of MT_RING entries
+    const uint32_t lds = mt_lds_bytes(W, a.L) + (staged ? MT_WIN * 4u * BLOCK + (MT_RING - MT_CHUNK) * entry * BLOCK : 0u);
     int bpc = 0;
     if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(fn), BLOCK, lds))
         return (int)e;
