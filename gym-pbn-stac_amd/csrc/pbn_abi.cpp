@@ -1106,7 +1106,7 @@ int pbn_mt_seed(pbn_batch* b, const uint64_t* seeds, int init_state) {
             if (seeds[e] >> 32) return fail(PBN_E_RANGE, "Seed must be between 0 and 2**32 - 1 (env %llu)",
                                             (unsigned long long)e);
     SET_DEV(b);
-    const size_t row = 4 * (size_t)MT_ROW * b->B;
+    const size_t row = 4 * ((size_t)MT_ROW * b->B + MT_TAIL_PAD);
     if (int rc = b->mt_py.ensure(row)) return rc;
     if (int rc = b->mt_pos_py.ensure(4 * b->B)) return rc;
     if (table) {

@@ -113,35 +113,44 @@ __global__ __launch_bounds__(BLOCK) void k_mt_seed(MTArgs a) {
 // resolved in the generation pass, MTDraw), so the buffer is 4 KiB and 6 workgroups fit a CU instead of 4:
 // 54.7 vs 50.0 G node-updates/s at 1M envs (profiles/r06_mt_mode_ab.json)
 constexpr uint32_t MT_CHUNK = 8;
-constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu, MT_A = 0x9908b0dfu;
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int WAIT_VM0 = 0x0F70, WAIT_VM0_LGKM0 = 0x0070, WAIT_LGKM0 = 0xC07F;
+constexpr uint32_t MT_UPPER = 0x80000000u, MT_A = 0x9908b0dfu;  // (lower mask: ~MT_UPPER)
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
-    const uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
-    return m ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+    // (a & UPPER) | (b & LOWER) and (y >> 1) ^ (A if y odd) as two v_bitop3 (0xE4: S0 where S2 else S1; 0x78:
+    // S0 ^ (S1 & S2)); y's low bit is b's
+    const uint32_t y = __builtin_amdgcn_bitop3_b32(a, b, MT_UPPER, 0xE4);
+    const uint32_t odd = 0u - (b & 1u);
+    return m ^ __builtin_amdgcn_bitop3_b32(y >> 1, odd, MT_A, 0x78);
 }
 
 // Twist one row in place, all 64 lanes of the wave active (row: wave-uniform). Returns new word `lane` of the row.
 __device__ __forceinline__ uint32_t mt_twist_coop(uint32_t* __restrict__ row, uint32_t lane) {
     uint32_t o1[4], p1[4], m1[4], o2[4], p2[4], o3[3], p3[3];
-    // every load unconditional (indices clamped into the row; the clamped lanes' words are never stored), so all
-    // 26 are in flight together: conditional loads became a branch and a round trip each
+    // every load unconditional and at a fixed offset from one address (row + lane), so all 26 are in flight
+    // together without per-load address arithmetic (conditional loads became a branch and a round trip each).
+    // Lanes past a phase's range read up to 29 words past the row -- the next env's row, or the table's tail pad
+    // (MT_TAIL_PAD) after the last -- and never store them.
+    const uint32_t* const r = row + lane;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const uint32_t k1 = min(lane + 64u * j, 226u), k2 = 227u + k1;
-        o1[j] = row[k1];
-        p1[j] = row[k1 + 1u];
-        m1[j] = row[k1 + 397u];
-        o2[j] = row[k2];
-        p2[j] = row[k2 + 1u];
+        o1[j] = r[64 * j];
+        p1[j] = r[64 * j + 1];
+        m1[j] = r[64 * j + 397];
+        o2[j] = r[64 * j + 227];
+        p2[j] = r[64 * j + 228];
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const uint32_t k3 = min(454u + lane + 64u * j, 623u);
-        o3[j] = row[k3];
-        p3[j] = row[min(k3 + 1u, 623u)];
+        o3[j] = r[454 + 64 * j];
+        p3[j] = r[455 + 64 * j];
     }
-    // every old word is read before any new word is written (other lanes read what this lane overwrites)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every old word is read before any new word is written (other lanes read what this lane overwrites). As the
+    // builtin, so the compiler knows every load before it (LDS-DMA windows too) is done and adds no wait for them
+    // ahead of later LDS reads (an asm wait is opaque to it)
+    __builtin_amdgcn_s_waitcnt(WAIT_VM0);
+    asm volatile("" ::: "memory");
     uint32_t n1[4], n2[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -430,25 +439,37 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                     // new words go to its owner's window from the twisting lanes' registers.
                     const bool tw = need && pos >= MT_N;
                     uint64_t mask = __ballot(tw);
+                    const bool twisted = mask != 0ull;
                     if (tw) pos = 0;
                     base = pos & ~3u;
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    // the window's previous reads done; a previous pass's twist stores done before any row is read
+                    __builtin_amdgcn_s_waitcnt(WAIT_VM0_LGKM0);
+                    asm volatile("" ::: "memory");
                     if (!tw) {
 #pragma unroll
                         for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
                             __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u),
                                                              16, 0, 0);
                     }
-                    while (mask) {
-                        const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-                        mask &= mask - 1ull;
-                        const uint32_t nw = mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
-                        if (lane < MT_WIN) *reinterpret_cast<uint32_t*>(win + (lane >> 2) * 1024u + L * 16u + (lane & 3u) * 4u) = nw;
-                        // the row's later windows are staged from what the other lanes wrote (k_mt_step's fence)
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (twisted) {
+                        // (a do-while: the compiler then knows a twist's wait retired the windows' loads)
+                        do {
+                            const uint32_t L = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+                            mask &= mask - 1ull;
+                            const uint32_t nw = mt_twist_coop(a.mt_py + (e0 + L) * MT_ROW, lane);
+                            if (lane < MT_WIN)
+                                *reinterpret_cast<uint32_t*>(win + (lane >> 2) * 1024u + L * 16u + (lane & 3u) * 4u) = nw;
+                            // the row's later windows are staged from what the other lanes wrote (k_mt_step's fence)
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        } while (mask);
+                        // the windows' loads are done (the twist waited for them before its stores); its stores are
+                        // left in flight until the next pass, which waits for them before it reads a row
+                        __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+                    } else {
+                        __builtin_amdgcn_s_waitcnt(WAIT_VM0_LGKM0);
                     }
-                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                    asm volatile("" ::: "memory");
                     end = min(base + MT_WIN, MT_N);
                 }
                 uint32_t wn = word(min(pos - base, MT_WIN - 1u));  // the next word, read an iteration ahead
@@ -492,7 +513,7 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
             for (uint32_t c = 0; c < tgt; ++c) {
                 const uint32_t d = dbuf[((rd + c) & (MT_RING - 1u)) * BLOCK];
                 const uint32_t i = d & 511u, dw = i >> 5, sh = i & 31u;
-                const uint64_t rec = recs[i * a.L.pmax + (d >> 9)];
+                const uint64_t rec = recs[__umul24(i, a.L.pmax) + (d >> 9)];  // 24-bit multiply: full rate
                 const uint32_t self = P.get(dw);
                 P.put(dw, (self & ~(1u << sh)) | (predictor_apply(P, i, self, rec) << sh));
             }

@@ -160,6 +160,7 @@ constexpr uint32_t GPOOL_CU_WORD = 16, GPOOL_CTL_BYTES = 4u * (GPOOL_CU_WORD + 1
 constexpr uint32_t GPOOL_MIN_CAP = 16384;
 
 constexpr uint32_t MT_ROW = 624;
+constexpr uint32_t MT_TAIL_PAD = 64;  // words allocated past the last row (the twist's unconditional loads read up to 29)
 
 // 1 / log2(1-p) from a geometric-gap table T_k = floor((1-p)^k 2^32) (host side): taken at the
 // largest k whose T_k keeps >= 20 significant bits; 0 when every T_k is tiny (p ~ 1).
