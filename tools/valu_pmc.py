@@ -112,7 +112,7 @@ def main():
                     "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " --kernel-trace on tools/valu_pmc_child.py"}
     doc = {"kernels": res, "valu_peak": "256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s "
                                         "(MI355X_MICROARCH.md: chip parameters, wave scheduling)"}
-    (ROOT / "gpurun_out" / f"r05_{SET}_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
+    (ROOT / "gpurun_out" / f"r06_{SET}_pmc.json").write_text(json.dumps(doc, indent=1) + "\n")
     print(json.dumps({k: {kk: v for kk, v in r.items() if kk not in ("counters", "source", "kernel")}
                       for k, r in res.items()}))
 
