@@ -398,7 +398,7 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     uint8_t* const win = lds + a.L.bytes + 8u * W * BLOCK + (uint32_t)sizeof(D) * MT_RING * BLOCK + (threadIdx.x >> 6) * (MT_WIN * 256u);
     const uint32_t lane = __lane_id();
     const uint32_t* const mine = reinterpret_cast<const uint32_t*>(win + lane * 16u);
-    auto word = [&](uint32_t k) { return mine[(k >> 2) * 256u + (k & 3u)]; };  // window word k (< MT_WIN)
+    const uint32_t win_ofs = (uint32_t)(reinterpret_cast<const uint8_t*>(mine) - lds);  // this lane's granule 0
     const uint64_t* const recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
     const ulonglong2* const thr4 = reinterpret_cast<const ulonglong2*>(lds + a.L.off_thr);
     const uint32_t N = (uint32_t)a.L.n_nodes;
@@ -422,6 +422,12 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
         // to slot `wr`; every phase applies MT_APPLY per lane, oldest first (slot `rd`, the same in every lane)
         uint32_t pend = 0, wr = 0, rd = 0;
         uint32_t base = pos & ~3u, end = 0;  // the lane's window [base, end) of its row; none staged yet
+        // row word p of the window at LDS byte wc + 4 p + 1008 (p >> 2) (granule (p - base) / 4 at 1 KiB steps, the
+        // word at 4 B): three ops per word from pos, no clamp (p = end reads the pad granule after the windows)
+        uint32_t wc = 0;
+        auto wword = [&](uint32_t p) {
+            return *reinterpret_cast<const uint32_t*>(lds + (__umul24(p >> 2, 1008u) + wc + (p << 2)));
+        };
         while (__ballot(left > 0u) != 0ull) {
             const uint32_t tgt = min(left, MT_APPLY);
             const uint32_t cap = min(left, MT_RING);  // never a draw past this launch's T
@@ -471,23 +477,27 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                     }
                     asm volatile("" ::: "memory");
                     end = min(base + MT_WIN, MT_N);
+                    wc = win_ofs - (base << 2) - (base >> 2) * 1008u;
                 }
-                uint32_t wn = word(min(pos - base, MT_WIN - 1u));  // the next word, read an iteration ahead
+                uint32_t wn = wword(pos);  // the next word, read an iteration ahead
                 ulonglong2 t0{}, t1{};
                 if constexpr (TP4) {
                     t0 = thr4[2u * node];
                     t1 = thr4[2u * node + 1u];
                 }
-                // walk while a lane that needs draws has words; a lane with room in its ring walks along
-                while (__ballot(need && pos < end) != 0ull) {
+                // walk while a lane that needs draws has words; a lane with room in its ring walks along (as the AND
+                // of two compares' lane masks: __ballot(need && pos < end) turned the mask into 0 / 1 and back)
+                while ((__builtin_amdgcn_ballot_w64(pos < end) & __builtin_amdgcn_ballot_w64(pend < tgt)) != 0ull) {
                     // the machine as selects (one divergent branch, the draw's store, instead of three)
                     const bool act = can && pos < end;
                     const uint32_t w = mt_temper(wn);
                     pos += act ? 1u : 0u;
-                    wn = word(min(pos - base, MT_WIN - 1u));
+                    wn = wword(pos);
                     const uint32_t r = w >> ks;  // _randbelow: rejected if >= N
                     const bool take_node = act && stt == 0u && r < N, take_wa = act && stt == 1u, emit = act && stt == 2u;
-                    const uint64_t k53 = k53_of(wa, w);
+                    // k53 = (wa >> 5) << 26 | w >> 6 as its two halves, the low one ({wa >> 5, w} >> 6) by one v_alignbit
+                    // (three ops; the 64-bit shift and OR took four)
+                    const uint64_t k53 = ((uint64_t)(wa >> 11) << 32) | __builtin_amdgcn_alignbit(wa >> 5, w, 6);
                     uint32_t choice;
                     if constexpr (TP4)
                         choice = (k53 >= t0.x ? 1u : 0u) + (k53 >= t0.y ? 1u : 0u) + (k53 >= t1.x ? 1u : 0u) +
@@ -501,7 +511,6 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                     stt = take_node ? 1u : take_wa ? 2u : emit ? 0u : stt;
                     pend += emit ? 1u : 0u;
                     wr = (wr + (emit ? 1u : 0u)) & (MT_RING - 1u);
-                    need = pend < tgt;
                     can = pend < cap;
                     if constexpr (TP4) {  // the next iteration's thresholds, read an iteration ahead like its word
                         t0 = thr4[2u * node];
@@ -586,7 +595,8 @@ int launch_mt_step(int W, const MTArgs& a, int n_cu, void* stream) {
                                                : mt_step_fn<KIND_PREDICTOR_MIX, false>(W);
     if (!fn) return (int)hipErrorInvalidValue;
     const uint32_t entry = mt_wide(a.L) ? 4u : 2u;  // staged: MT_WIN-word windows, a ring of MT_RING entries
-    const uint32_t lds = mt_lds_bytes(W, a.L) + (staged ? MT_WIN * 4u * BLOCK + (MT_RING - MT_CHUNK) * entry * BLOCK : 0u);
+    // (staged: + one granule row after the last wave's windows, read by a lane at the end of its window)
+    const uint32_t lds = mt_lds_bytes(W, a.L) + (staged ? MT_WIN * 4u * BLOCK + (MT_RING - MT_CHUNK) * entry * BLOCK + 1024u : 0u);
     int bpc = 0;
     if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(fn), BLOCK, lds))
         return (int)e;
