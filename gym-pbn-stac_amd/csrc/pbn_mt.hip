@@ -390,7 +390,22 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     typedef __attribute__((address_space(1))) uint32_t g32;
     typedef __attribute__((address_space(3))) uint32_t l32;
     extern __shared__ __align__(16) uint8_t lds[];
-    stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    if constexpr (TP4) {
+        // the thresholds re-expressed on X = wa << 32 | w, the draw's two words as they come: k53(X) = (wa >> 5) 2^26 +
+        // (w >> 6) is monotone in X, so k53 >= T <=> X >= X_T, X_T = (T >> 26) << 37 | (T mod 2^26) << 6 (the smallest
+        // such X); a threshold past every k53 (padding, T >= 2^53) becomes 2^64 - 1, above every X the walk forms (its
+        // bit 0 cleared: same k53). The compare then needs no k53 (three ops per draw)
+        stage_image(reinterpret_cast<const uint4*>(a.img) + a.L.off_rec / 16, (a.L.bytes - a.L.off_rec) / 16,
+                    reinterpret_cast<uint4*>(lds) + a.L.off_rec / 16);
+        const uint64_t* const gthr = reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a.img) + a.L.off_thr);
+        uint64_t* const xthr = reinterpret_cast<uint64_t*>(lds + a.L.off_thr);
+        for (uint32_t k = threadIdx.x; k < 4u * (uint32_t)a.L.n_nodes; k += BLOCK) {
+            const uint64_t t = gthr[k];
+            xthr[k] = t >= (1ull << 53) ? ~0ull : ((t >> 26) << 37) | ((t & 0x3FFFFFFull) << 6);
+        }
+    } else {
+        stage_image(reinterpret_cast<const uint4*>(a.img), a.L.bytes / 16, reinterpret_cast<uint4*>(lds));
+    }
     __syncthreads();
     const Plane P{reinterpret_cast<uint32_t*>(lds + a.L.bytes) + threadIdx.x};
     D* const dbuf = reinterpret_cast<D*>(lds + a.L.bytes + 8u * W * BLOCK) + threadIdx.x;  // [MT_RING][BLOCK]
@@ -495,15 +510,15 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                     wn = wword(pos);
                     const uint32_t r = w >> ks;  // _randbelow: rejected if >= N
                     const bool take_node = act && stt == 0u && r < N, take_wa = act && stt == 1u, emit = act && stt == 2u;
-                    // k53 = (wa >> 5) << 26 | w >> 6 as its two halves, the low one ({wa >> 5, w} >> 6) by one v_alignbit
-                    // (three ops; the 64-bit shift and OR took four)
-                    const uint64_t k53 = ((uint64_t)(wa >> 11) << 32) | __builtin_amdgcn_alignbit(wa >> 5, w, 6);
                     uint32_t choice;
-                    if constexpr (TP4)
-                        choice = (k53 >= t0.x ? 1u : 0u) + (k53 >= t0.y ? 1u : 0u) + (k53 >= t1.x ? 1u : 0u) +
-                                 (k53 >= t1.y ? 1u : 0u);
-                    else
+                    if constexpr (TP4) {  // the X-space thresholds (prologue)
+                        const uint64_t X = ((uint64_t)wa << 32) | (w & ~1u);
+                        choice = (X >= t0.x ? 1u : 0u) + (X >= t0.y ? 1u : 0u) + (X >= t1.x ? 1u : 0u) + (X >= t1.y ? 1u : 0u);
+                    } else {
+                        // k53 = (wa >> 5) << 26 | w >> 6 as its two halves, the low one ({wa >> 5, w} >> 6) by v_alignbit
+                        const uint64_t k53 = ((uint64_t)(wa >> 11) << 32) | __builtin_amdgcn_alignbit(wa >> 5, w, 6);
                         choice = predictor_choice(node, k53, lds, a.L);
+                    }
                     const uint32_t ent = node | (choice << 9);
                     if (emit) dbuf[wr * BLOCK] = (D)ent;  // (unconditional, into a spare slot: 84.6 vs 87.3 G)
                     node = take_node ? r : node;
