@@ -379,6 +379,9 @@ constexpr uint32_t MT_APPLY = PBN_MT_APPLY;
 #define PBN_MT_RING 16  // ring / apply 8 / 8: 78.6 G, 16 / 8: 85.8, 16 / 4: 84.7, 16 / 12: 82.4, 32 / 16: 85.6 (W 12)
 #endif
 constexpr uint32_t MT_RING = PBN_MT_RING;  // draw entries per lane in the ring
+#ifndef PBN_MT_WALK_UNROLL
+#define PBN_MT_WALK_UNROLL 4  // 1 / 2 / 3 / 4: 94.1 / 94.3 / 92.5 / 94.2 G at 1M envs, 51.4 / 53.9 / 51.7 / 54.9 G at 65k
+#endif
 static_assert(MT_APPLY >= 1u && MT_APPLY <= MT_RING && MT_RING >= MT_CHUNK && (MT_RING & (MT_RING - 1u)) == 0u,
               "ring of a power of two");
 
@@ -502,7 +505,9 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                 }
                 // walk while a lane that needs draws has words; a lane with room in its ring walks along (as the AND
                 // of two compares' lane masks: __ballot(need && pos < end) turned the mask into 0 / 1 and back)
-                while ((__builtin_amdgcn_ballot_w64(pos < end) & __builtin_amdgcn_ballot_w64(pend < tgt)) != 0ull) {
+                // (PBN_MT_WALK_UNROLL words per test: a word walked after the wave's last needy lane ran out is a lane
+                // with ring room walking along, or no lane at all -- the same draws, made earlier)
+                auto walk1 = [&]() {
                     // the machine as selects (one divergent branch, the draw's store, instead of three)
                     const bool act = can && pos < end;
                     const uint32_t w = mt_temper(wn);
@@ -531,6 +536,10 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                         t0 = thr4[2u * node];
                         t1 = thr4[2u * node + 1u];
                     }
+                };
+                while ((__builtin_amdgcn_ballot_w64(pos < end) & __builtin_amdgcn_ballot_w64(pend < tgt)) != 0ull) {
+#pragma unroll
+                    for (int k = 0; k < PBN_MT_WALK_UNROLL; ++k) walk1();
                 }
             }
             // apply the phase: every lane its tgt oldest draws
