@@ -390,7 +390,6 @@ static_assert(MT_APPLY >= 1u && MT_APPLY <= MT_RING && MT_RING >= MT_CHUNK && (M
 template <int W, bool WIDE, bool TP4>
 __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     using D = MTDraw<KIND_PREDICTOR_MIX, WIDE>;
-    typedef __attribute__((address_space(1))) uint32_t g32;
     typedef __attribute__((address_space(3))) uint32_t l32;
     extern __shared__ __align__(16) uint8_t lds[];
     if constexpr (TP4) {
@@ -417,6 +416,7 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
     const uint32_t lane = __lane_id();
     const uint32_t* const mine = reinterpret_cast<const uint32_t*>(win + lane * 16u);
     const uint32_t win_ofs = (uint32_t)(reinterpret_cast<const uint8_t*>(mine) - lds);  // this lane's granule 0
+    const uint32_t win_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(l32*)win);
     const uint64_t* const recs = reinterpret_cast<const uint64_t*>(lds + a.L.off_rec);
     const ulonglong2* const thr4 = reinterpret_cast<const ulonglong2*>(lds + a.L.off_thr);
     const uint32_t N = (uint32_t)a.L.n_nodes;
@@ -472,8 +472,13 @@ __global__ __launch_bounds__(BLOCK) void k_mt_staged(MTArgs a) {
                     if (!tw) {
 #pragma unroll
                         for (uint32_t j = 0; j < MT_WIN / 4u; ++j)
-                            __builtin_amdgcn_global_load_lds((g32*)(row + min(base + 4u * j, MT_N - 4u)), (l32*)(win + j * 1024u),
-                                                             16, 0, 0);
+                            // the LDS-DMA as asm (m0 = the granule row's LDS address): for the builtin the compiler
+                            // waited vmcnt(0) ahead of the walk's threshold reads (LDS it could not prove disjoint), i.e.
+                            // for a twist's stores left in flight (+1 %, profiles/r06_mt_valu_trim_ab.json); the kernel
+                            // waits for these itself (the refill's and the twist's s_waitcnt)
+                            asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(row + min(base + 4u * j, MT_N - 4u)),
+                                         "{m0}"(win_lds + j * 1024u)
+                                         : "memory");
                     }
                     if (twisted) {
                         // (a do-while: the compiler then knows a twist's wait retired the windows' loads)
